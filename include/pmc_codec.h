@@ -1,0 +1,123 @@
+/*
+ * pmc_codec.h -- C-ABI of the MI355X-native value codec (libpmc_codec.so).
+ *
+ * Drop-in boundary for the reference's src/compressor.  The reference
+ * exposes two static C++ methods, called only from src/kvs:
+ *   GzipCompressor::Compress(const char*)            /root/reference/src/compressor/gzip_compressor.hpp:37
+ *                                                     (impl gzip_compressor.cpp:3-50; caller kvs.cpp:183)
+ *   GzipCompressor::Decompress(const char*, size_t)  /root/reference/src/compressor/gzip_compressor.hpp:43
+ *                                                     (impl gzip_compressor.cpp:52-111; caller kvs.cpp:233)
+ * The reference links them at build time (no FFI); poor-man-s-cache_amd/dropin/
+ * gzip_compressor.{hpp,cpp} re-implements that class on top of this ABI so src/kvs links
+ * unchanged.  Everything here is plain pointers and sizes; no torch or HIP types appear
+ * in the signatures (streams are passed as void* = hipStream_t).
+ *
+ * Output bytes are bit-identical to the reference Compress (zlib 1.2.11, level 9,
+ * windowBits 15+16, memLevel 8, default strategy) on the same input bytes.
+ *
+ * Return codes mirror the reference (gzip_compressor.hpp:10-12) and zlib:
+ */
+#ifndef PMC_CODEC_H
+#define PMC_CODEC_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PMC_OK 0                 /* OPERATION_SUCCESS (gzip_compressor.hpp:12)            */
+#define PMC_INVALID_INPUT (-999) /* INVALID_INPUT: null or empty (gzip_compressor.hpp:11) */
+#define PMC_Z_DATA_ERROR (-3)    /* corrupt stream, CRC/ISIZE mismatch, not gzip           */
+#define PMC_Z_MEM_ERROR (-4)     /* device allocation failed                               */
+#define PMC_Z_BUF_ERROR (-5)     /* truncated stream (reference hangs here)     */
+#define PMC_E_NO_DEVICE (-100)   /* no usable gfx950 device / HIP runtime error            */
+#define PMC_E_CAPACITY (-101)    /* output capacity too small (batched API only)           */
+#define PMC_E_ARG (-102)         /* invalid argument                                       */
+
+typedef struct pmc_ctx pmc_ctx; /* one device + streams + scratch; not thread-safe */
+
+/* Create a context on HIP device `device` (gfx950).  Returns PMC_OK or PMC_E_NO_DEVICE. */
+int pmc_ctx_create(int device, pmc_ctx **out);
+void pmc_ctx_destroy(pmc_ctx *ctx);
+/* Default context (device 0), created on first use; used by the drop-in. */
+pmc_ctx *pmc_default_ctx(void);
+const char *pmc_last_error(void);
+/* Library version string and the device arch it was built for ("gfx950"). */
+const char *pmc_version(void);
+
+/* Worst-case gzip member size for an input of `len` bytes. */
+size_t pmc_gzip_bound(size_t len);
+
+/* ---- single value, host memory (what GzipCompressor::Compress/Decompress wrap) ----
+ * pmc_gzip_compress: compress in[0..in_len) into out (capacity out_cap >= pmc_gzip_bound).
+ *   in_len == 0 or in == NULL -> PMC_INVALID_INPUT (gzip_compressor.cpp:4).
+ * pmc_gzip_decompress: decompress one gzip member; *out_len receives the size.  The
+ *   caller sizes `out` from pmc_gzip_isize(); PMC_E_CAPACITY if the stream is longer. */
+int pmc_gzip_compress(pmc_ctx *ctx, const void *in, size_t in_len, void *out, size_t out_cap,
+                      size_t *out_len);
+int pmc_gzip_decompress(pmc_ctx *ctx, const void *in, size_t in_len, void *out, size_t out_cap,
+                        size_t *out_len);
+/* ISIZE trailer of a gzip member (last 4 bytes, little endian); 0 if in_len < 18. */
+uint32_t pmc_gzip_isize(const void *in, size_t in_len);
+
+/* ---- batched, DEVICE-resident (the hot path) ------------------------------------------
+ * Value i occupies src[src_off[i] .. src_off[i]+src_len[i]); its gzip member is written to
+ * dst[dst_off[i] ..), at most dst_cap[i] bytes, its length to dst_len[i] and its status to
+ * rc[i].  All arrays are device pointers; the call only enqueues work on `stream`
+ * (hipStream_t, NULL = legacy default stream) and returns.  max_len is an upper bound on
+ * src_len[] (for compress) or on the decompressed sizes (for decompress); it selects the
+ * kernel variant (LDS-resident vs HBM-resident working set).  Values are independent, so
+ * any batch may be split arbitrarily (across calls, streams or GPUs).
+ * Compress: src_len[i] == 0 -> rc PMC_INVALID_INPUT (reference semantics).  Input bytes
+ *   may contain NULs (binary safe; the single-value drop-in keeps the reference's strlen).
+ * Decompress: dst_cap[i] must be >= the decompressed size (ISIZE); use
+ *   pmc_gzip_isize_batch to read the trailers on device. */
+int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                            const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
+                            const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
+                            void *stream);
+int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                              const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
+                              const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
+                              void *stream);
+/* isize[i] = ISIZE trailer of member i (0 if src_len[i] < 18). */
+int pmc_gzip_isize_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                         const uint32_t *src_len, uint32_t n, uint32_t *isize, void *stream);
+
+/* ---- batched, HOST-resident (what a batched server path would call) --------------------
+ * Same layout, all pointers in host memory.  Stages through pinned buffers with
+ * hipMemcpyAsync H2D -> kernel -> D2H on the context's stream and waits for completion.
+ * dst_off may be NULL: outputs are then packed back to back in dst (dst_off[i] = sum of
+ * previous dst_cap[]). */
+int pmc_gzip_compress_batch_host(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                 const uint32_t *src_len, uint32_t n, uint8_t *dst,
+                                 const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+                                 int32_t *rc);
+int pmc_gzip_decompress_batch_host(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                   const uint32_t *src_len, uint32_t n, uint8_t *dst,
+                                   const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+                                   int32_t *rc);
+
+/* ---- benchmark / test helpers (device, enqueue only) -----------------------------------
+ * Synthetic values of SURVEY.md §8d: value i of vlen bytes written to dst + i*vlen, with
+ * global index idx = index ? index[i] : first+i.  kind 0 = slice of corpus at
+ * splitmix64(seed ^ idx) % (corpus_len-vlen+1); kind 1 = random [A-Za-z0-9] (8-byte group g:
+ * splitmix64(splitmix64(seed ^ idx) + g)).  corpus and index are device pointers. */
+int pmc_gen_values(const uint8_t *corpus, uint32_t corpus_len, uint64_t seed, int kind, uint64_t first,
+                   const uint64_t *index, uint32_t n, uint32_t vlen, uint8_t *dst, void *stream);
+/* Fixed-stride layout: off[i] = i*stride, len[i] = vlen (device arrays). */
+int pmc_fill_layout(uint64_t *off, uint32_t *len, uint32_t *cap, uint32_t n, uint64_t stride,
+                    uint32_t vlen, uint32_t capv, void *stream);
+/* mismatches[0] += number of values whose bytes differ between a and b (device). */
+int pmc_compare_values(const uint8_t *a, const uint64_t *a_off, const uint8_t *b, const uint64_t *b_off,
+                       const uint32_t *len, const uint32_t *len_b, uint32_t n, uint32_t *mismatches,
+                       void *stream);
+/* shard routing: gpu[i] = MurmurHash3_x64_128("key"+(first+i), seed 0)[0]
+ * % num_shards % n_gpus  (hash.cpp:4-9 routing, server.cpp:113,121,132). */
+int pmc_route_keys(uint64_t first, uint32_t n, uint32_t num_shards, uint32_t n_gpus, uint8_t *gpu,
+                   void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,159 @@
+"""ctypes bindings for the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this
+module, and only as the checker (never as the thing measured or shipped).
+
+liboracle.so  : CPU restatement of zlib 1.2.11 level-9 gzip (see pmc_oracle.h).
+_ref/libref_gzip.so : the reference's own GzipCompressor
+                  (/root/reference/src/compressor/gzip_compressor.cpp) built by
+                  `make -C oracle ref`; optional (absent if the reference was not
+                  present when it was built).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+_REF = None
+
+
+def build(ref=True):
+    subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
+    if ref and os.path.isdir("/root/reference"):
+        subprocess.check_call(["make", "-s", "-C", HERE, "ref"])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build(ref=False)
+        L = ctypes.CDLL(path)
+        L.oracle_gzip_bound.restype = ctypes.c_size_t
+        L.oracle_gzip_bound.argtypes = [ctypes.c_size_t]
+        for fn in (L.oracle_gzip_compress, L.oracle_gzip_compress_dp):
+            fn.restype = ctypes.c_size_t
+            fn.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.oracle_gzip_decompress.restype = ctypes.c_int
+        L.oracle_gzip_decompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
+                                             ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+        L.oracle_crc32.restype = ctypes.c_uint32
+        L.oracle_crc32.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_splitmix64.restype = ctypes.c_uint64
+        L.oracle_splitmix64.argtypes = [ctypes.c_uint64]
+        L.oracle_gen_values.restype = None
+        L.oracle_gen_values.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
+                                        ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+        _LIB = L
+    return _LIB
+
+
+def bound(n):
+    return lib().oracle_gzip_bound(n)
+
+
+def compress(data: bytes, dp=False) -> bytes:
+    L = lib()
+    out = ctypes.create_string_buffer(L.oracle_gzip_bound(len(data)))
+    fn = L.oracle_gzip_compress_dp if dp else L.oracle_gzip_compress
+    n = fn(data, len(data), out)
+    return out.raw[:n]
+
+
+def isize(gz: bytes) -> int:
+    return int.from_bytes(gz[-4:], "little") if len(gz) >= 4 else 0
+
+
+def decompress(gz: bytes, cap=None):
+    """Returns (rc, bytes).  rc: 0, -3 (Z_DATA_ERROR), -5 (truncated)."""
+    L = lib()
+    if cap is None:
+        cap = max(isize(gz), 1) + 64
+    out = ctypes.create_string_buffer(cap)
+    n = ctypes.c_size_t(0)
+    rc = L.oracle_gzip_decompress(gz, len(gz), out, cap, ctypes.byref(n))
+    return rc, (out.raw[:n.value] if rc == 0 else b"")
+
+
+def crc32(data: bytes, crc=0) -> int:
+    return lib().oracle_crc32(crc, data, len(data))
+
+
+class _Stats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in (
+        "positions", "searches", "candidates", "literals", "matches", "blocks",
+        "stored_blocks", "fixed_blocks", "dynamic_blocks")]
+
+
+def last_stats():
+    s = _Stats()
+    lib().oracle_get_stats(ctypes.byref(s))
+    return {k: getattr(s, k) for k, _ in s._fields_}
+
+
+def gen_values(corpus: bytes, seed: int, kind: int, first: int, n: int, vlen: int) -> np.ndarray:
+    out = np.empty((n, vlen), dtype=np.uint8)
+    lib().oracle_gen_values(corpus, len(corpus), seed, kind, first, n, vlen,
+                            out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+# ---------------------------------------------------------------- reference (_ref)
+def ref_available():
+    return os.path.exists(os.path.join(HERE, "_ref", "libref_gzip.so"))
+
+
+def ref():
+    global _REF
+    if _REF is None:
+        R = ctypes.CDLL(os.path.join(HERE, "_ref", "libref_gzip.so"))
+        R.ref_compress.restype = ctypes.c_int
+        R.ref_compress.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p),
+                                   ctypes.POINTER(ctypes.c_size_t)]
+        R.ref_decompress.restype = ctypes.c_int
+        R.ref_decompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]
+        R.ref_free.argtypes = [ctypes.c_void_p]
+        R.ref_zlib_version.restype = ctypes.c_char_p
+        R.ref_bench.restype = ctypes.c_int
+        R.ref_bench.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(ctypes.c_uint64)]
+        _REF = R
+    return _REF
+
+
+def ref_compress(s: bytes):
+    """The reference GzipCompressor::Compress (strlen semantics).  Returns (rc, bytes)."""
+    R = ref()
+    p = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    rc = R.ref_compress(s, ctypes.byref(p), ctypes.byref(n))
+    data = ctypes.string_at(p.value, n.value) if p.value else b""
+    if p.value:
+        R.ref_free(p)
+    return rc, data
+
+
+def ref_decompress(gz: bytes):
+    """The reference GzipCompressor::Decompress.  Never call on truncated input (hangs)."""
+    R = ref()
+    p = ctypes.c_void_p()
+    rc = R.ref_decompress(gz, len(gz), ctypes.byref(p))
+    data = ctypes.string_at(p.value) if p.value else None
+    if p.value:
+        R.ref_free(p)
+    return rc, data
+
+
+def ref_bench(values: np.ndarray, nthreads: int):
+    R = ref()
+    n, vlen = values.shape
+    tc, td = ctypes.c_double(), ctypes.c_double()
+    cb = ctypes.c_uint64()
+    bad = R.ref_bench(values.ctypes.data_as(ctypes.c_void_p), n, vlen, nthreads,
+                      ctypes.byref(tc), ctypes.byref(td), ctypes.byref(cb))
+    return {"t_compress": tc.value, "t_decompress": td.value, "compressed_bytes": cb.value, "bad": bad}

@@ -1,0 +1,72 @@
+// ref_shim.cpp -- TEST INFRASTRUCTURE ONLY (oracle/_ref).
+//
+// C entry points around the reference's own GzipCompressor, compiled straight from
+// /root/reference/src/compressor/gzip_compressor.cpp by oracle/Makefile (target _ref).
+// Used (a) by tests/golden/make_golden.py to produce the committed golden vectors and
+// (b) by bench.py's cpu_baseline leg ("kind": "reference"): the reference codec timed
+// on the host cores, one value per call exactly as src/kvs calls it
+// (/root/reference/src/kvs/kvs.cpp:183,233).
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "gzip_compressor.hpp"
+
+extern "C" {
+
+int ref_compress(const char *in, char **out, size_t *out_len) {
+    CompressResult r = GzipCompressor::Compress(in);
+    *out = r.data;
+    *out_len = r.size;
+    return r.operationResult;
+}
+
+int ref_decompress(const char *in, size_t in_len, char **out) {
+    DecompressResult r = GzipCompressor::Decompress(in, in_len);
+    *out = r.data;
+    return r.operationResult;
+}
+
+void ref_free(char *p) { delete[] p; }
+
+const char *ref_zlib_version(void) { return zlibVersion(); }
+
+// Times Compress over n values of vlen bytes (NUL-free; each copied into a NUL-terminated
+// buffer first, outside the timed region), then Decompress over the results.
+// Values are dealt round-robin to nthreads std::threads.
+int ref_bench(const uint8_t *values, uint32_t n, uint32_t vlen, int nthreads, double *t_comp,
+              double *t_decomp, uint64_t *comp_bytes) {
+    std::vector<std::vector<char>> src(n);
+    for (uint32_t i = 0; i < n; i++) {
+        src[i].resize(vlen + 1);
+        memcpy(src[i].data(), values + (uint64_t)i * vlen, vlen);
+        src[i][vlen] = 0;
+    }
+    std::vector<CompressResult> comp(n);
+    std::atomic<int> bad{0};
+    auto run = [&](auto &&fn) {
+        std::vector<std::thread> th;
+        auto t0 = std::chrono::steady_clock::now();
+        for (int t = 0; t < nthreads; t++)
+            th.emplace_back([&, t] {
+                for (uint32_t i = t; i < n; i += nthreads) fn(i);
+            });
+        for (auto &x : th) x.join();
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    };
+    *t_comp = run([&](uint32_t i) { comp[i] = GzipCompressor::Compress(src[i].data()); });
+    uint64_t cb = 0;
+    for (auto &c : comp) cb += c.size;
+    *comp_bytes = cb;
+    *t_decomp = run([&](uint32_t i) {
+        DecompressResult d = GzipCompressor::Decompress(comp[i].data, comp[i].size);
+        if (d.operationResult != 0 || memcmp(d.data, src[i].data(), vlen + 1) != 0) bad++;
+        delete[] d.data;
+    });
+    for (auto &c : comp) delete[] c.data;
+    return bad.load();
+}
+}

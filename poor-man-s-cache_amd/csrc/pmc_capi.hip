@@ -1,0 +1,524 @@
+// pmc_capi.hip -- host side of the C-ABI declared in include/pmc_codec.h.
+//
+// Owns per-device state (stream, symbol slabs, HBM working sets, pinned staging) and
+// turns a batch into at most two launches per direction: the LDS-resident kernel for
+// values whose working set fits a wave's LDS share, and the HBM-resident variant for
+// the rest (large values; same device code, working set in a per-wave HBM slab).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/pmc_codec.h"
+#include "pmc_device.hpp"
+#include "pmc_kernels.hpp"
+
+#define PMC_API extern "C" __attribute__((visibility("default")))
+
+namespace pmc {
+
+__constant__ Tables c_tables = make_tables();
+__constant__ uint32_t c_crc_table[256];
+__constant__ uint32_t c_crc_shift16[kCrcShiftEntries];
+__constant__ uint32_t c_crc_shift64k[kCrcShiftEntries];
+
+static thread_local std::string g_err;
+static void set_err(const char *what, hipError_t e) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: %s", what, e == hipSuccess ? "" : hipGetErrorString(e));
+    g_err = buf;
+}
+#define HIP_TRY(x)                    \
+    do {                              \
+        hipError_t e_ = (x);          \
+        if (e_ != hipSuccess) {       \
+            set_err(#x, e_);          \
+            return PMC_E_NO_DEVICE;   \
+        }                             \
+    } while (0)
+
+// ---- CRC-32 constants (zlib crc32.c / 1.2.12 crc32_combine_gen) -------------------------
+static uint32_t h_multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (;;) {
+        if (a & m) {
+            p ^= b;
+            if ((a & (m - 1)) == 0) break;
+        }
+        m >>= 1;
+        b = b & 1 ? (b >> 1) ^ kCrcPoly : b >> 1;
+    }
+    return p;
+}
+static uint32_t h_x2nmodp(uint64_t n, unsigned k) { // x^(n * 2^k) mod P
+    uint32_t x2n[64];
+    uint32_t p = 1u << 30; // x^1
+    x2n[0] = p;
+    for (int i = 1; i < 64; i++) x2n[i] = p = h_multmodp(p, p);
+    p = 1u << 31; // x^0
+    while (n) {
+        if (n & 1) p = h_multmodp(x2n[k & 63], p);
+        n >>= 1;
+        k++;
+    }
+    return p;
+}
+
+static int upload_constants() {
+    uint32_t tab[256];
+    for (uint32_t n = 0; n < 256; n++) {
+        uint32_t c = n;
+        for (int k = 0; k < 8; k++) c = c & 1 ? kCrcPoly ^ (c >> 1) : c >> 1;
+        tab[n] = c;
+    }
+    static uint32_t s16[kCrcShiftEntries], s64k[kCrcShiftEntries];
+    // x^(8*16*d) = x^(d * 2^7);  x^(8*65536*d) = x^(d * 2^19)
+    for (int d = 0; d < kCrcShiftEntries; d++) {
+        s16[d] = h_x2nmodp((uint64_t)d, 7);
+        s64k[d] = h_x2nmodp((uint64_t)d, 19);
+    }
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_table), tab, sizeof tab));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_shift16), s16, sizeof s16));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_shift64k), s64k, sizeof s64k));
+    return PMC_OK;
+}
+
+constexpr uint64_t kLdsPerCu = 160 * 1024;
+constexpr uint64_t kCrcTabBytes = 1024;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return PMC_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max(n, (size_t)4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            set_err("hipMalloc", e);
+            return PMC_Z_MEM_ERROR;
+        }
+        cap = want;
+        return PMC_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+struct HostBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return PMC_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max(n, (size_t)4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            set_err("hipHostMalloc", e);
+            return PMC_Z_MEM_ERROR;
+        }
+        cap = want;
+        return PMC_OK;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+} // namespace pmc
+
+using namespace pmc;
+
+struct pmc_ctx {
+    int device = 0;
+    int cus = 0;
+    hipStream_t stream = nullptr;
+    DevBuf tokens, dscratch;     // deflate symbol slabs / HBM working sets
+    DevBuf staging;              // device side of host-API calls
+    HostBuf pinned;              // host side of host-API calls
+};
+
+namespace {
+
+struct Launch {
+    int wpb;        // waves per block
+    int blocks;     // grid size
+    uint64_t wave_bytes;
+    size_t lds;     // dynamic LDS per block
+};
+
+int occupancy_blocks(const void *kernel, int threads, size_t lds) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, lds) != hipSuccess || nb < 1) nb = 1;
+    return nb;
+}
+
+// values with len <= this go through the LDS deflate kernel (one wave needs the whole
+// working set: value, sorted keys, ranks, output image, Huffman trees)
+uint64_t deflate_lds_limit() {
+    uint64_t lo = 64, hi = 65535;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi + 1) / 2;
+        if (deflate_wave_bytes(false, mid) + kCrcTabBytes <= kLdsPerCu) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+Launch plan_lds(pmc_ctx *ctx, const void *kernel, uint64_t wave_bytes, uint64_t n_items) {
+    Launch L;
+    L.wave_bytes = wave_bytes;
+    uint64_t fit = (kLdsPerCu - kCrcTabBytes) / wave_bytes;
+    L.wpb = (int)std::max<uint64_t>(1, std::min<uint64_t>(4, fit));
+    L.lds = kCrcTabBytes + L.wpb * wave_bytes;
+    int per_cu = occupancy_blocks(kernel, 64 * L.wpb, L.lds);
+    uint64_t need_blocks = (n_items + L.wpb - 1) / L.wpb;
+    L.blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * per_cu, need_blocks));
+    return L;
+}
+
+} // namespace
+
+// ================================================================== API
+PMC_API const char *pmc_last_error(void) { return g_err.c_str(); }
+PMC_API const char *pmc_version(void) { return "pmc_codec 0.1 gfx950 (zlib-1.2.11 level-9 gzip, bit-exact)"; }
+PMC_API size_t pmc_gzip_bound(size_t len) { return (size_t)gzip_bound(len); }
+
+PMC_API int pmc_ctx_create(int device, pmc_ctx **out) {
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= device) {
+        set_err("hipGetDeviceCount", e);
+        return PMC_E_NO_DEVICE;
+    }
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        g_err = std::string("device is ") + prop.gcnArchName + ", library built for gfx950";
+        return PMC_E_NO_DEVICE;
+    }
+    int rc = upload_constants();
+    if (rc) return rc;
+    // the LDS-resident kernels may use the whole 160 KiB of a CU
+    HIP_TRY(hipFuncSetAttribute((const void *)deflate_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kLdsPerCu));
+    HIP_TRY(hipFuncSetAttribute((const void *)inflate_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kLdsPerCu));
+    HIP_TRY(hipFuncSetAttribute((const void *)inflate_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kLdsPerCu));
+    pmc_ctx *c = new pmc_ctx;
+    c->device = device;
+    c->cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return PMC_E_NO_DEVICE;
+    }
+    *out = c;
+    return PMC_OK;
+}
+
+PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->tokens.release();
+    c->dscratch.release();
+    c->staging.release();
+    c->pinned.release();
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+PMC_API pmc_ctx *pmc_default_ctx(void) {
+    static std::once_flag once;
+    static pmc_ctx *ctx = nullptr;
+    std::call_once(once, [] {
+        if (pmc_ctx_create(0, &ctx) != PMC_OK) ctx = nullptr;
+    });
+    return ctx;
+}
+
+PMC_API uint32_t pmc_gzip_isize(const void *in, size_t in_len) {
+    if (!in || in_len < 18) return 0;
+    const uint8_t *p = (const uint8_t *)in + in_len - 4;
+    return p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                    const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
+                                    const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
+                                    void *stream) {
+    if (!ctx) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    hipStream_t st = (hipStream_t)stream;
+    DeflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, nullptr};
+    const uint64_t lim = deflate_lds_limit();
+    a.lds_max_len = std::min<uint64_t>(lim, std::max<uint64_t>(max_len, 1));
+    // ---- LDS kernel (values <= lds_max_len) ----
+    {
+        uint64_t cap = (a.lds_max_len + 63) & ~(uint64_t)63;
+        if (cap > lim) cap = lim;
+        a.cap_len = cap;
+        uint64_t wb = deflate_wave_bytes(false, cap);
+        Launch L = plan_lds(ctx, (const void *)deflate_kernel<false>, wb, n);
+        a.wave_bytes = wb;
+        uint64_t waves = (uint64_t)L.blocks * L.wpb;
+        int r = ctx->tokens.ensure(waves * kSlabSyms * sizeof(uint32_t));
+        if (r) return r;
+        a.tokens = (uint32_t *)ctx->tokens.p;
+        hipLaunchKernelGGL(deflate_kernel<false>, dim3(L.blocks), dim3(64 * L.wpb), L.lds, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            set_err("deflate_kernel<lds>", e);
+            return PMC_E_NO_DEVICE;
+        }
+    }
+    // ---- HBM kernel (values > lds_max_len) ----
+    if (max_len > a.lds_max_len) {
+        a.cap_len = max_len;
+        uint64_t wb = deflate_wave_bytes(true, max_len);
+        uint64_t waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 2,
+                                                                  (8ull << 30) / std::max<uint64_t>(wb, 1)));
+        waves = std::min<uint64_t>(waves, n);
+        int r = ctx->dscratch.ensure(waves * wb);
+        if (r) return r;
+        r = ctx->tokens.ensure(std::max<uint64_t>(waves, ctx->tokens.cap / (kSlabSyms * 4)) * kSlabSyms * 4);
+        if (r) return r;
+        a.wave_bytes = wb;
+        a.scratch = (uint8_t *)ctx->dscratch.p;
+        a.tokens = (uint32_t *)ctx->tokens.p;
+        hipLaunchKernelGGL(deflate_kernel<true>, dim3((unsigned)waves), dim3(64), kCrcTabBytes, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            set_err("deflate_kernel<hbm>", e);
+            return PMC_E_NO_DEVICE;
+        }
+    }
+    return PMC_OK;
+}
+
+static uint64_t inflate_lds_out_limit() { return 48 * 1024; }
+
+PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                      const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
+                                      const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
+                                      void *stream) {
+    if (!ctx) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    hipStream_t st = (hipStream_t)stream;
+    InflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr};
+    // output image capacity for the LDS kernel; the compressed input of a member whose
+    // output fits is at most gzip_bound(out) unless it is not a deflate member at all
+    uint64_t out_cap = std::min<uint64_t>(inflate_lds_out_limit(), std::max<uint64_t>(max_len, 1));
+    out_cap = (out_cap + 63) & ~(uint64_t)63;
+    a.lds_max_out = out_cap;
+    a.lds_max_in = gzip_bound(out_cap) + 64;
+    {
+        uint64_t wb = inflate_wave_bytes(false, a.lds_max_out, a.lds_max_in);
+        Launch L = plan_lds(ctx, (const void *)inflate_kernel<false>, wb, n);
+        a.wave_bytes = wb;
+        hipLaunchKernelGGL(inflate_kernel<false>, dim3(L.blocks), dim3(64 * L.wpb), L.lds, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            set_err("inflate_kernel<lds>", e);
+            return PMC_E_NO_DEVICE;
+        }
+    }
+    // members whose output or input exceeds the LDS image (rare: large values, or garbage
+    // input longer than its ISIZE suggests) -> HBM variant; always launched because input
+    // lengths are device-resident (the kernel skips members the LDS kernel handled)
+    {
+        uint64_t wb = inflate_wave_bytes(true, 0, 0);
+        uint64_t waves = std::min<uint64_t>((uint64_t)ctx->cus * 4, n);
+        a.wave_bytes = wb;
+        hipLaunchKernelGGL(inflate_kernel<true>, dim3((unsigned)((waves + 3) / 4)), dim3(256),
+                           kCrcTabBytes + 4 * wb, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            set_err("inflate_kernel<hbm>", e);
+            return PMC_E_NO_DEVICE;
+        }
+    }
+    return PMC_OK;
+}
+
+PMC_API int pmc_gzip_isize_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                 const uint32_t *src_len, uint32_t n, uint32_t *isize, void *stream) {
+    if (!ctx) return PMC_E_ARG;
+    if (!n) return PMC_OK;
+    hipLaunchKernelGGL(isize_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                       (hipStream_t)stream, src, src_off, src_len, n, isize);
+    return hipGetLastError() == hipSuccess ? PMC_OK : PMC_E_NO_DEVICE;
+}
+
+// ---- host-resident batches: pinned staging, H2D -> kernels -> D2H -------------------
+namespace {
+enum Dir { kCompress, kDecompress };
+
+int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+               uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+               int32_t *rc) {
+    if (!ctx) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    // packed device layout: src bytes back to back, dst slots back to back
+    uint64_t in_bytes = 0, out_bytes = 0, max_len = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        in_bytes += src_len[i];
+        out_bytes += dst_cap[i];
+        uint64_t m = dir == kCompress ? src_len[i] : dst_cap[i];
+        max_len = std::max(max_len, m);
+    }
+    auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    const uint64_t meta = al(n * 8ull) * 2 + al(n * 4ull) * 4;
+    const uint64_t total = meta + al(in_bytes + 16) + al(out_bytes + 16);
+    int r = ctx->pinned.ensure(total);
+    if (r) return r;
+    r = ctx->staging.ensure(total);
+    if (r) return r;
+    uint8_t *hp = (uint8_t *)ctx->pinned.p, *dp = (uint8_t *)ctx->staging.p;
+    uint64_t o = 0;
+    uint64_t *h_soff = (uint64_t *)(hp + o), *d_soff = (uint64_t *)(dp + o);
+    o += al(n * 8ull);
+    uint64_t *h_doff = (uint64_t *)(hp + o), *d_doff = (uint64_t *)(dp + o);
+    o += al(n * 8ull);
+    uint32_t *h_slen = (uint32_t *)(hp + o), *d_slen = (uint32_t *)(dp + o);
+    o += al(n * 4ull);
+    uint32_t *h_dcap = (uint32_t *)(hp + o), *d_dcap = (uint32_t *)(dp + o);
+    o += al(n * 4ull);
+    uint32_t *h_dlen = (uint32_t *)(hp + o), *d_dlen = (uint32_t *)(dp + o);
+    o += al(n * 4ull);
+    int32_t *h_rc = (int32_t *)(hp + o), *d_rc = (int32_t *)(dp + o);
+    o += al(n * 4ull);
+    uint8_t *h_src = hp + o, *d_src = dp + o;
+    o += al(in_bytes + 16);
+    uint8_t *h_dst = hp + o, *d_dst = dp + o;
+    uint64_t so = 0, doff = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        h_soff[i] = so;
+        h_slen[i] = src_len[i];
+        memcpy(h_src + so, src + src_off[i], src_len[i]);
+        so += src_len[i];
+        h_doff[i] = doff;
+        h_dcap[i] = dst_cap[i];
+        doff += dst_cap[i];
+    }
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(dp, hp, meta, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_src, h_src, in_bytes, hipMemcpyHostToDevice, st));
+    r = dir == kCompress
+            ? pmc_gzip_compress_batch(ctx, d_src, d_soff, d_slen, n, d_dst, d_doff, d_dcap, d_dlen, d_rc,
+                                      (uint32_t)max_len, st)
+            : pmc_gzip_decompress_batch(ctx, d_src, d_soff, d_slen, n, d_dst, d_doff, d_dcap, d_dlen, d_rc,
+                                        (uint32_t)max_len, st);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(h_dlen, d_dlen, al(n * 4ull) * 2, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h_dst, d_dst, out_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    uint64_t po = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint64_t to = dst_off ? dst_off[i] : po;
+        rc[i] = h_rc[i];
+        dst_len[i] = h_dlen[i];
+        if (h_rc[i] == 0) memcpy(dst + to, h_dst + h_doff[i], h_dlen[i]);
+        po += dst_cap[i];
+    }
+    return PMC_OK;
+}
+} // namespace
+
+PMC_API int pmc_gzip_compress_batch_host(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                         const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
+                                         const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc) {
+    return host_batch(ctx, kCompress, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc);
+}
+
+PMC_API int pmc_gzip_decompress_batch_host(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                           const uint32_t *src_len, uint32_t n, uint8_t *dst,
+                                           const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+                                           int32_t *rc) {
+    return host_batch(ctx, kDecompress, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc);
+}
+
+PMC_API int pmc_gzip_compress(pmc_ctx *ctx, const void *in, size_t in_len, void *out, size_t out_cap,
+                              size_t *out_len) {
+    *out_len = 0;
+    if (!in || in_len == 0) return PMC_INVALID_INPUT;
+    if (!ctx) ctx = pmc_default_ctx();
+    if (!ctx) return PMC_E_NO_DEVICE;
+    if (in_len > 0xffffffffull || out_cap < pmc_gzip_bound(in_len)) return PMC_E_CAPACITY;
+    uint64_t so = 0;
+    uint32_t sl = (uint32_t)in_len, cap = (uint32_t)std::min<size_t>(out_cap, 0xffffffffull), dl = 0;
+    int32_t rc = 0;
+    int r = host_batch(ctx, kCompress, (const uint8_t *)in, &so, &sl, 1, (uint8_t *)out, &so, &cap, &dl, &rc);
+    if (r) return r;
+    *out_len = dl;
+    return rc;
+}
+
+PMC_API int pmc_gzip_decompress(pmc_ctx *ctx, const void *in, size_t in_len, void *out, size_t out_cap,
+                                size_t *out_len) {
+    *out_len = 0;
+    if (!in || in_len == 0) return PMC_INVALID_INPUT;
+    if (!ctx) ctx = pmc_default_ctx();
+    if (!ctx) return PMC_E_NO_DEVICE;
+    uint64_t so = 0;
+    uint32_t sl = (uint32_t)in_len, cap = (uint32_t)std::min<size_t>(out_cap, 0xffffffffull), dl = 0;
+    int32_t rc = 0;
+    int r = host_batch(ctx, kDecompress, (const uint8_t *)in, &so, &sl, 1, (uint8_t *)out, &so, &cap, &dl, &rc);
+    if (r) return r;
+    *out_len = dl;
+    return rc;
+}
+
+// ---- helpers -------------------------------------------------------------------------
+static dim3 grid_for(uint64_t items, int per_thread = 1) {
+    uint64_t b = (items / per_thread + 255) / 256;
+    return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, 1u << 16)));
+}
+
+PMC_API int pmc_gen_values(const uint8_t *corpus, uint32_t corpus_len, uint64_t seed, int kind, uint64_t first,
+                           const uint64_t *index, uint32_t n, uint32_t vlen, uint8_t *dst, void *stream) {
+    if (!n || !vlen || (kind == 0 && vlen > corpus_len)) return PMC_E_ARG;
+    hipLaunchKernelGGL(gen_values_kernel, grid_for((uint64_t)n * ((vlen + 7) / 8)), dim3(256), 0,
+                       (hipStream_t)stream, corpus, corpus_len, seed, kind, first, index, n, vlen, dst);
+    return hipGetLastError() == hipSuccess ? PMC_OK : PMC_E_NO_DEVICE;
+}
+
+PMC_API int pmc_fill_layout(uint64_t *off, uint32_t *len, uint32_t *cap, uint32_t n, uint64_t stride, uint32_t vlen,
+                            uint32_t capv, void *stream) {
+    if (!n) return PMC_OK;
+    hipLaunchKernelGGL(fill_layout_kernel, grid_for(n), dim3(256), 0, (hipStream_t)stream, off, len, cap, n, stride,
+                       vlen, capv);
+    return hipGetLastError() == hipSuccess ? PMC_OK : PMC_E_NO_DEVICE;
+}
+
+PMC_API int pmc_compare_values(const uint8_t *a, const uint64_t *a_off, const uint8_t *b, const uint64_t *b_off,
+                               const uint32_t *len, const uint32_t *len_b, uint32_t n, uint32_t *mismatches,
+                               void *stream) {
+    if (!n) return PMC_OK;
+    hipLaunchKernelGGL(compare_values_kernel, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0,
+                       (hipStream_t)stream, a, a_off, b, b_off, len, len_b, n, mismatches);
+    return hipGetLastError() == hipSuccess ? PMC_OK : PMC_E_NO_DEVICE;
+}
+
+PMC_API int pmc_route_keys(uint64_t first, uint32_t n, uint32_t num_shards, uint32_t n_gpus, uint8_t *gpu,
+                           void *stream) {
+    if (!n || !num_shards || !n_gpus) return PMC_E_ARG;
+    hipLaunchKernelGGL(route_kernel, grid_for(n), dim3(256), 0, (hipStream_t)stream, first, n, num_shards, n_gpus,
+                       gpu);
+    return hipGetLastError() == hipSuccess ? PMC_OK : PMC_E_NO_DEVICE;
+}

@@ -1,0 +1,129 @@
+// pmc_device.hpp -- gfx950 device primitives shared by the codec kernels.
+//
+// Wave64 helpers (ballot / shuffle reductions / scans), the zlib constant tables in
+// __constant__ memory, and a lane-parallel CRC-32 (the gzip trailer checksum zlib's
+// read_buf folds in, deflate.c / crc32.c) for a byte string resident in LDS or HBM.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pmc_trees.hpp"
+
+namespace pmc {
+
+constexpr int kWave = 64;
+constexpr uint32_t kCrcPoly = 0xEDB88320u;
+constexpr int kCrcShiftEntries = 4096; // x^(128*d) mod P for d < 4096 (16-byte steps)
+
+// zlib trees.c static tables (make_tables() is constexpr; copied once at load time).
+extern __constant__ Tables c_tables;
+extern __constant__ uint32_t c_crc_table[256];
+extern __constant__ uint32_t c_crc_shift16[kCrcShiftEntries];  // x^(8*16*d)   mod P
+extern __constant__ uint32_t c_crc_shift64k[kCrcShiftEntries]; // x^(8*65536*d) mod P
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+    uint32_t lo = rfl((uint32_t)v), hi = rfl((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Intra-wave ordering point for LDS/global hand-offs between lanes of one wave.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// Ordering point strong enough for per-wave scratch in global memory (waits for stores).
+__device__ __forceinline__ void wave_sync_global() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint32_t t = __shfl_xor(v, o);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_xor_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
+    return v;
+}
+// inclusive prefix sum across the wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    int l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
+    int l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint64_t t = __shfl_up(v, o);
+        if (l >= o) v += t;
+    }
+    return v;
+}
+
+// GF(2) product a*b mod P in the reflected CRC-32 domain (zlib 1.2.12 multmodp).
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll 8
+    for (int k = 31; k >= 0; k--) {
+        p ^= ((a >> k) & 1u) ? b : 0u;
+        b = (b >> 1) ^ (kCrcPoly & (0u - (b & 1u)));
+    }
+    return p;
+}
+
+// x^(8*16*d) mod P for any chunk distance d.
+__device__ __forceinline__ uint32_t crc_shift_chunks(uint32_t d) {
+    uint32_t k = c_crc_shift16[d & (kCrcShiftEntries - 1)];
+    if (d >= (uint32_t)kCrcShiftEntries) k = multmodp(k, c_crc_shift64k[d >> 12]);
+    return k;
+}
+
+// CRC-32 of buf[0..len) computed by the whole wave.  The message is cut into 16-byte
+// chunks aligned from its END (chunk d covers [len-16(d+1), len-16d)); lane l takes
+// chunks d = l, l+64, ...  Each chunk's register (from 0, or from 0xFFFFFFFF for the
+// chunk holding byte 0) is shifted past the d*16 bytes that follow it by one GF(2)
+// multiply with x^(128 d) mod P, and the wave XOR-reduces.  By linearity of the CRC
+// register this equals the serial crc32().  `tab` is a 256-entry table (LDS).
+template <class BytePtr>
+__device__ inline uint32_t wave_crc32(BytePtr buf, uint32_t len, const uint32_t *tab) {
+    uint32_t nchunks = (len + 15) >> 4;
+    uint32_t acc = 0;
+    for (uint32_t d = (uint32_t)lane_id(); d < nchunks; d += 64) {
+        int64_t end = (int64_t)len - 16 * (int64_t)d;
+        int64_t beg = end - 16;
+        uint32_t c = 0;
+        if (beg <= 0) {
+            beg = 0;
+            c = 0xFFFFFFFFu;
+        }
+        for (int64_t k = beg; k < end; k++) c = tab[(c ^ buf[k]) & 0xff] ^ (c >> 8);
+        acc ^= d ? multmodp(crc_shift_chunks(d), c) : c;
+    }
+    acc = wave_xor_u32(acc);
+    if (len == 0) return 0;
+    return ~acc;
+}
+
+} // namespace pmc

@@ -1,0 +1,564 @@
+// pmc_inflate.hip -- batched gzip decompression on gfx950.
+//
+// Replaces GzipCompressor::Decompress (/root/reference/src/compressor/gzip_compressor.cpp:52-111,
+// called from src/kvs/kvs.cpp:233) for many independent gzip members at once, with the
+// validation verdicts of zlib 1.2.11 inflateInit2(15+16) (see oracle/inflate.c for the
+// rule list): -3 for any corruption / CRC / ISIZE mismatch, -5 for truncated input (the
+// reference hangs there), 0 on success.
+//
+// One wave64 per member (persistent grid).  Per member:
+//   1. stage the compressed bytes in LDS (coalesced), lane 0 parses the gzip header
+//   2. per block: stored -> lane-parallel copy; fixed/dynamic -> decode tables in LDS
+//      (9-bit root lookup, canonical fallback for longer codes; built by the wave)
+//   3. lane 0 decodes up to 64 tokens (literal / length+distance) into LDS; the wave then
+//      materialises them: all literals of the batch in parallel, then each match copied
+//      lane-parallel (period replication when distance < length)
+//   4. CRC-32 of the output lane-parallel, ISIZE check, copy-out to HBM.
+// Members whose output does not fit the LDS image use the same code with the output
+// image written straight into dst (kHbm variant).
+#include <hip/hip_runtime.h>
+
+#include "pmc_device.hpp"
+#include "pmc_kernels.hpp"
+
+namespace pmc {
+
+constexpr int kRootBits = 9;
+constexpr uint16_t kEntLong = 0xFFFF, kEntInvalid = 0xFFFE;
+
+__constant__ uint16_t c_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27,
+                                     31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t c_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193,
+                                     257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t c_cl_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// Canonical decoder for one code (zlib inftrees semantics for validity).
+struct Huff {
+    uint16_t count[16];
+    uint16_t offs[16];
+    uint16_t symbol[288];
+    uint16_t fast[1 << kRootBits]; // sym | len << 9, kEntLong, kEntInvalid
+    int32_t max;                   // longest code length, 0 = no codes
+    int32_t pad_;
+};
+
+struct InflateScratch {
+    Huff lit, dist, cl;
+    uint16_t lens[320];
+    uint32_t tok[64];  // literal: byte; match: 1<<31 | (dist-1)<<8 | (len-3)
+    uint32_t tpos[64]; // output position of each token (low 32 bits of the running count)
+    int32_t status[4]; // [0] batch status from lane 0
+};
+
+__host__ __device__ inline uint64_t a16(uint64_t x) { return (x + 15) & ~(uint64_t)15; }
+
+struct InflateLayout {
+    uint64_t scr, in, out, total;
+};
+template <bool kHbm>
+__host__ __device__ inline InflateLayout inflate_layout(uint64_t max_out, uint64_t max_in) {
+    InflateLayout L;
+    uint64_t off = 0;
+    L.scr = off;
+    off += a16(sizeof(InflateScratch));
+    L.in = off;
+    off += kHbm ? 0 : a16(max_in + 32);
+    L.out = off;
+    off += kHbm ? 0 : a16(max_out + 16);
+    L.total = a16(off);
+    return L;
+}
+uint64_t inflate_wave_bytes(bool hbm, uint64_t max_out, uint64_t max_in) {
+    return hbm ? inflate_layout<true>(max_out, max_in).total : inflate_layout<false>(max_out, max_in).total;
+}
+
+// Build count/offs/symbol (lane 0) and the fast table (wave).  Returns 0 or -1 (inftrees
+// over-subscribed / incomplete rule); is_codes selects the stricter code-length-code rule.
+__device__ inline int huff_build(Huff &h, const uint16_t *lens, int n, bool is_codes) {
+    const int l = lane_id();
+    int bad = 0;
+    if (l == 0) {
+        for (int k = 0; k < 16; k++) h.count[k] = 0;
+        for (int s = 0; s < n; s++) h.count[lens[s]]++;
+        int mx = 0;
+        for (int len = 15; len >= 1; len--)
+            if (h.count[len]) {
+                mx = len;
+                break;
+            }
+        h.max = mx;
+        if (mx) {
+            int left = 1;
+            for (int len = 1; len <= 15; len++) {
+                left <<= 1;
+                left -= h.count[len];
+                if (left < 0) bad = 1;
+            }
+            if (!bad && left > 0 && (is_codes || mx != 1)) bad = 1;
+            h.offs[1] = 0;
+            for (int len = 1; len < 15; len++) h.offs[len + 1] = (uint16_t)(h.offs[len] + h.count[len]);
+            uint16_t o[16];
+            for (int k = 0; k < 16; k++) o[k] = h.offs[k];
+            for (int s = 0; s < n; s++)
+                if (lens[s]) h.symbol[o[lens[s]]++] = (uint16_t)s;
+        }
+    }
+    wave_sync();
+    bad = rfl(bad);
+    if (bad) return -1;
+    const int mx = rfl(h.max);
+    // every root entry starts invalid (incomplete codes, or no codes at all)
+    for (int e = l; e < (1 << kRootBits); e += 64) h.fast[e] = kEntInvalid;
+    wave_sync();
+    if (mx == 0) return 0;
+    // canonical code of the j-th symbol of length L: first[L] + (j - offs[L])
+    uint32_t nsym = h.offs[15] + h.count[15];
+    for (uint32_t j = l; j < nsym; j += 64) {
+        int s = h.symbol[j];
+        int L = lens[s];
+        uint32_t first = 0, code = 0;
+        for (int k = 1; k <= L; k++) { // first code of length k (canonical)
+            first = (first + (k > 1 ? h.count[k - 1] : 0)) << (k > 1 ? 1 : 0);
+        }
+        code = first + (j - h.offs[L]);
+        uint32_t rev = __builtin_bitreverse32(code) >> (32 - L);
+        if (L <= kRootBits) {
+            for (uint32_t e = rev; e < (1u << kRootBits); e += (1u << L)) h.fast[e] = (uint16_t)(s | (L << 9));
+        } else {
+            h.fast[rev & ((1u << kRootBits) - 1)] = kEntLong;
+        }
+    }
+    wave_sync();
+    return 0;
+}
+
+// Lane-0 bit reader over a byte stream with a truncation check.  kWords: the stream is
+// LDS-staged, 4-byte aligned and zero padded, so a 64-bit window is 3 aligned dwords;
+// otherwise (HBM variant) bytes are fetched individually with a bounds check.
+template <bool kWords>
+struct Bits {
+    const uint8_t *in;
+    uint64_t nbits; // total bits available
+    uint64_t pos;   // bits consumed
+    __device__ uint64_t peek64() const {
+        if (kWords) {
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(in);
+            uint64_t wi = pos >> 5;
+            uint32_t s = (uint32_t)(pos & 31);
+            uint64_t lo = ((uint64_t)w[wi + 1] << 32) | w[wi];
+            uint64_t v = lo >> s;
+            if (s) v |= (uint64_t)w[wi + 2] << (64 - s);
+            return v;
+        }
+        uint64_t byte = pos >> 3, nb = (nbits + 7) >> 3;
+        uint64_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            uint64_t bb = byte + k < nb ? in[byte + k] : 0;
+            v |= k < 8 ? bb << (8 * k) : 0;
+            if (k == 8 && (pos & 7)) v = (v >> (pos & 7)) | (bb << (64 - (pos & 7)));
+        }
+        return v;
+    }
+    __device__ bool need(uint64_t n) const { return pos + n <= nbits; }
+    __device__ uint32_t get(uint32_t n) {
+        uint32_t v = (uint32_t)(peek64() & ((n >= 32) ? 0xffffffffull : ((1ull << n) - 1)));
+        pos += n;
+        return v;
+    }
+};
+
+// Decode one symbol: >=0 symbol, -1 invalid, -2 truncated.
+template <bool kW>
+__device__ inline int decode_sym(Bits<kW> &br, const Huff &h) {
+    uint64_t w = br.peek64();
+    uint16_t e = h.fast[w & ((1u << kRootBits) - 1)];
+    if (e != kEntLong) {
+        if (e == kEntInvalid) {
+            if (!br.need(1)) return -2;
+            return -1;
+        }
+        uint32_t L = e >> 9;
+        if (!br.need(L)) return -2;
+        br.pos += L;
+        return e & 0x1ff;
+    }
+    int code = 0, first = 0, index = 0;
+    for (int len = 1; len <= 15; len++) {
+        code |= (int)((w >> (len - 1)) & 1);
+        int count = h.count[len];
+        if (code - count < first) {
+            if (!br.need((uint32_t)len)) return -2;
+            br.pos += (uint64_t)len;
+            return h.symbol[index + (code - first)];
+        }
+        index += count;
+        first += count;
+        first <<= 1;
+        code <<= 1;
+    }
+    return -1;
+}
+
+template <bool kHbm>
+struct InflateWave {
+    InflateScratch *sc;
+    uint8_t *inb; // staged input (LDS) or src (HBM variant)
+    uint8_t *out; // output image (LDS) or dst (HBM variant)
+    const uint32_t *crc_tab;
+
+    __device__ void sync() {
+        if (kHbm) wave_sync_global();
+        else wave_sync();
+    }
+
+    // materialise the token batch [0, nt): literals in parallel, then matches in order
+    __device__ void materialise(int nt, uint64_t base, uint64_t cap) {
+        const int l = lane_id();
+        if (l < nt) {
+            uint32_t t = sc->tok[l];
+            uint64_t p = base + sc->tpos[l];
+            if (!(t >> 31) && p < cap) out[p] = (uint8_t)t;
+        }
+        sync();
+        for (int j = 0; j < nt; j++) {
+            uint32_t t = sc->tok[j];
+            if (!(t >> 31)) continue;
+            const uint32_t len = (t & 0xff) + 3, dist = ((t >> 8) & 0x7fff) + 1;
+            uint64_t p = base + sc->tpos[j];
+            for (uint32_t k = l; k < len; k += 64) {
+                uint64_t sidx = dist >= len ? p - dist + k : p - dist + (k % dist);
+                if (p + k < cap) out[p + k] = sidx < cap ? out[sidx] : 0;
+            }
+            sync();
+        }
+    }
+
+    __device__ int run(const uint8_t *src, uint64_t in_len, uint8_t *dst, uint64_t cap, uint32_t *dst_len) {
+        const int l = lane_id();
+        // 1. stage input (zero padded)
+        if (!kHbm) {
+            const uint64_t padded = (in_len + 16) & ~(uint64_t)3;
+            uint32_t *iw = reinterpret_cast<uint32_t *>(inb);
+            if ((((uintptr_t)src) & 3) == 0) {
+                const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src);
+                uint64_t full = in_len >> 2;
+                for (uint64_t k = l; k < padded / 4; k += 64) iw[k] = k < full ? s4[k] : 0u;
+                sync();
+                if ((uint64_t)l < (in_len & 3)) inb[full * 4 + l] = src[full * 4 + l];
+            } else {
+                for (uint64_t k = l; k < padded / 4; k += 64) iw[k] = 0;
+                sync();
+                for (uint64_t k = l; k < in_len; k += 64) inb[k] = src[k];
+            }
+            sync();
+        }
+        // 2. gzip header (lane 0)
+        int hrc = 0;
+        uint64_t p = 0;
+        if (l == 0) {
+            const uint8_t *in = inb;
+            do {
+                if (in_len < 2) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                if (in[0] != 0x1f || in[1] != 0x8b) { hrc = PMC_Z_DATA_ERROR_DEV; break; }
+                if (in_len < 4) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                if (in[2] != 8) { hrc = PMC_Z_DATA_ERROR_DEV; break; }
+                uint32_t flg = in[3];
+                if (flg & 0xe0) { hrc = PMC_Z_DATA_ERROR_DEV; break; }
+                if (in_len < 10) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                p = 10;
+                if (flg & 0x04) {
+                    if (in_len < p + 2) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                    uint64_t xlen = in[p] | ((uint64_t)in[p + 1] << 8);
+                    p += 2;
+                    if (in_len < p + xlen) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                    p += xlen;
+                }
+                if (flg & 0x08) {
+                    while (p < in_len && in[p] != 0) p++;
+                    if (p >= in_len) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                    p++;
+                }
+                if (flg & 0x10) {
+                    while (p < in_len && in[p] != 0) p++;
+                    if (p >= in_len) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                    p++;
+                }
+                if (flg & 0x02) {
+                    if (in_len < p + 2) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                    uint32_t hc = in[p] | ((uint32_t)in[p + 1] << 8), c = 0xFFFFFFFFu;
+                    for (uint64_t k = 0; k < p; k++) c = crc_tab[(c ^ in[k]) & 0xff] ^ (c >> 8);
+                    if (hc != ((~c) & 0xffff)) { hrc = PMC_Z_DATA_ERROR_DEV; break; }
+                    p += 2;
+                }
+            } while (0);
+        }
+        hrc = rfl(hrc);
+        if (hrc) return hrc;
+        p = rfl64(p);
+        Bits<!kHbm> br{inb, in_len * 8, p * 8};
+        uint64_t outn = 0; // bytes produced (uniform)
+        int last = 0;
+        do {
+            // ---- block header (lane 0) ----
+            int type = 0, rc = 0;
+            if (l == 0) {
+                if (!br.need(3)) rc = PMC_Z_BUF_ERROR_DEV;
+                else {
+                    last = (int)br.get(1);
+                    type = (int)br.get(2);
+                }
+            }
+            rc = rfl(rc);
+            if (rc) return rc;
+            last = rfl(last);
+            type = rfl(type);
+            br.pos = rfl64(br.pos);
+            if (type == 0) {
+                // stored
+                uint32_t len = 0;
+                if (l == 0) {
+                    br.pos = (br.pos + 7) & ~(uint64_t)7;
+                    if (!br.need(32)) rc = PMC_Z_BUF_ERROR_DEV;
+                    else {
+                        len = br.get(16);
+                        uint32_t nlen = br.get(16);
+                        if (len != (nlen ^ 0xffff)) rc = PMC_Z_DATA_ERROR_DEV;
+                        else if (!br.need(8ull * len)) rc = PMC_Z_BUF_ERROR_DEV;
+                    }
+                }
+                rc = rfl(rc);
+                if (rc) return rc;
+                len = rfl(len);
+                br.pos = rfl64(br.pos);
+                const uint64_t ib = br.pos >> 3;
+                for (uint64_t k = l; k < len; k += 64)
+                    if (outn + k < cap) out[outn + k] = inb[ib + k];
+                outn += len;
+                br.pos += 8ull * len;
+                sync();
+                continue;
+            }
+            if (type == 3) return PMC_Z_DATA_ERROR_DEV;
+            if (type == 1) {
+                // fixed code lengths (inflate.c fixedtables)
+                for (int s = l; s < 320; s += 64) sc->lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+                sync();
+                huff_build(sc->lit, sc->lens, 288, false);
+                huff_build(sc->dist, sc->lens + 288, 32, false);
+            } else {
+                // dynamic: HLIT/HDIST/HCLEN, code-length code, then the code lengths
+                int nlen = 0, ndist = 0, ncode = 0;
+                if (l == 0) {
+                    if (!br.need(14)) rc = PMC_Z_BUF_ERROR_DEV;
+                    else {
+                        nlen = (int)br.get(5) + 257;
+                        ndist = (int)br.get(5) + 1;
+                        ncode = (int)br.get(4) + 4;
+                        if (nlen > 286 || ndist > 30) rc = PMC_Z_DATA_ERROR_DEV;
+                        else {
+                            int k;
+                            for (k = 0; k < ncode; k++) {
+                                if (!br.need(3)) {
+                                    rc = PMC_Z_BUF_ERROR_DEV;
+                                    break;
+                                }
+                                sc->lens[c_cl_order[k]] = (uint16_t)br.get(3);
+                            }
+                            for (; k < 19; k++) sc->lens[c_cl_order[k]] = 0;
+                        }
+                    }
+                }
+                rc = rfl(rc);
+                if (rc) return rc;
+                sync();
+                if (huff_build(sc->cl, sc->lens, 19, true)) return PMC_Z_DATA_ERROR_DEV;
+                nlen = rfl(nlen);
+                ndist = rfl(ndist);
+                if (l == 0) {
+                    const int clmax = sc->cl.max;
+                    int have = 0;
+                    while (have < nlen + ndist) {
+                        int sym;
+                        if (clmax == 0) {
+                            if (!br.need(1)) { rc = PMC_Z_BUF_ERROR_DEV; break; }
+                            br.pos += 1;
+                            sym = 0;
+                        } else {
+                            sym = decode_sym(br, sc->cl);
+                            if (sym == -2) { rc = PMC_Z_BUF_ERROR_DEV; break; }
+                            if (sym < 0) { rc = PMC_Z_DATA_ERROR_DEV; break; }
+                        }
+                        if (sym < 16) {
+                            sc->lens[have++] = (uint16_t)sym;
+                        } else {
+                            uint32_t len = 0, copy;
+                            if (sym == 16) {
+                                if (!br.need(2)) { rc = PMC_Z_BUF_ERROR_DEV; break; }
+                                if (have == 0) { rc = PMC_Z_DATA_ERROR_DEV; break; }
+                                len = sc->lens[have - 1];
+                                copy = 3 + br.get(2);
+                            } else if (sym == 17) {
+                                if (!br.need(3)) { rc = PMC_Z_BUF_ERROR_DEV; break; }
+                                copy = 3 + br.get(3);
+                            } else {
+                                if (!br.need(7)) { rc = PMC_Z_BUF_ERROR_DEV; break; }
+                                copy = 11 + br.get(7);
+                            }
+                            if (have + (int)copy > nlen + ndist) { rc = PMC_Z_DATA_ERROR_DEV; break; }
+                            while (copy--) sc->lens[have++] = (uint16_t)len;
+                        }
+                    }
+                    if (!rc && sc->lens[256] == 0) rc = PMC_Z_DATA_ERROR_DEV;
+                    // move distance lengths to lens[288..]
+                    if (!rc) {
+                        for (int k = ndist - 1; k >= 0; k--) sc->lens[288 + k] = sc->lens[nlen + k];
+                        for (int k = nlen; k < 288; k++) sc->lens[k] = 0;
+                    }
+                }
+                rc = rfl(rc);
+                if (rc) return rc;
+                br.pos = rfl64(br.pos);
+                sync();
+                if (huff_build(sc->lit, sc->lens, nlen, false)) return PMC_Z_DATA_ERROR_DEV;
+                if (huff_build(sc->dist, sc->lens + 288, ndist, false)) return PMC_Z_DATA_ERROR_DEV;
+            }
+            // ---- symbol decode (lane 0) + materialisation (wave) ----
+            for (;;) {
+                int nt = 0, st = 0; // st: 0 more, 1 end of block, <0 error
+                uint32_t rel = 0;
+                if (l == 0) {
+                    const uint64_t o0 = outn;
+                    uint64_t o = outn;
+                    while (nt < 64) {
+                        int sym = decode_sym(br, sc->lit);
+                        if (sym == -2) { st = PMC_Z_BUF_ERROR_DEV; break; }
+                        if (sym < 0) { st = PMC_Z_DATA_ERROR_DEV; break; }
+                        if (sym < 256) {
+                            sc->tok[nt] = (uint32_t)sym;
+                            sc->tpos[nt] = (uint32_t)(o - o0);
+                            nt++;
+                            o++;
+                            continue;
+                        }
+                        if (sym == 256) { st = 1; break; }
+                        sym -= 257;
+                        if (sym >= 29) { st = PMC_Z_DATA_ERROR_DEV; break; }
+                        if (!br.need(c_lext[sym])) { st = PMC_Z_BUF_ERROR_DEV; break; }
+                        uint32_t len = c_lbase[sym] + br.get(c_lext[sym]);
+                        int ds = decode_sym(br, sc->dist);
+                        if (ds == -2) { st = PMC_Z_BUF_ERROR_DEV; break; }
+                        if (ds < 0 || ds >= 30) { st = PMC_Z_DATA_ERROR_DEV; break; }
+                        if (!br.need(c_dext[ds])) { st = PMC_Z_BUF_ERROR_DEV; break; }
+                        uint32_t dist = c_dbase[ds] + br.get(c_dext[ds]);
+                        if (dist > o) { st = PMC_Z_DATA_ERROR_DEV; break; }
+                        // match token: bit 31 | (dist-1) << 8 | (len-3)
+                        sc->tok[nt] = 0x80000000u | (dist - 1) << 8 | (len - 3);
+                        sc->tpos[nt] = (uint32_t)(o - o0);
+                        nt++;
+                        o += len;
+                    }
+                    rel = (uint32_t)(o - o0);
+                }
+                nt = rfl(nt);
+                st = rfl(st);
+                rel = rfl(rel);
+                br.pos = rfl64(br.pos);
+                sync();
+                materialise(nt, outn, cap);
+                outn += rel;
+                if (st < 0) return st;
+                if (st == 1) break;
+            }
+        } while (!last);
+        // 3. trailer: CRC-32 then ISIZE (inflate.c CHECK / LENGTH)
+        uint64_t tp = (br.pos + 7) >> 3;
+        if (in_len < tp + 4) return PMC_Z_BUF_ERROR_DEV;
+        if (outn > cap) return PMC_Z_DATA_ERROR_DEV;
+        sync();
+        uint32_t crc = wave_crc32(out, (uint32_t)outn, crc_tab);
+        uint32_t want = inb[tp] | ((uint32_t)inb[tp + 1] << 8) | ((uint32_t)inb[tp + 2] << 16) | ((uint32_t)inb[tp + 3] << 24);
+        if (crc != want) return PMC_Z_DATA_ERROR_DEV;
+        if (in_len < tp + 8) return PMC_Z_BUF_ERROR_DEV;
+        uint32_t isz = inb[tp + 4] | ((uint32_t)inb[tp + 5] << 8) | ((uint32_t)inb[tp + 6] << 16) | ((uint32_t)inb[tp + 7] << 24);
+        if (isz != (uint32_t)outn) return PMC_Z_DATA_ERROR_DEV;
+        // 4. copy-out
+        if (!kHbm) {
+            if ((((uintptr_t)dst) & 3) == 0) {
+                uint32_t *d4 = reinterpret_cast<uint32_t *>(dst);
+                const uint32_t *o4 = reinterpret_cast<const uint32_t *>(out);
+                uint64_t full = outn >> 2;
+                for (uint64_t k = l; k < full; k += 64) d4[k] = o4[k];
+                if ((uint64_t)l < (outn & 3)) dst[full * 4 + l] = out[full * 4 + l];
+            } else {
+                for (uint64_t k = l; k < outn; k += 64) dst[k] = out[k];
+            }
+        }
+        if (l == 0) *dst_len = (uint32_t)outn;
+        return 0;
+    }
+};
+
+template <bool kHbm>
+__global__ void __launch_bounds__(256) inflate_kernel(InflateArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
+    __syncthreads();
+    const int waves_per_block = blockDim.x / 64;
+    const int wib = threadIdx.x / 64;
+    const uint64_t wave = (uint64_t)blockIdx.x * waves_per_block + wib;
+    const uint64_t nwaves = (uint64_t)gridDim.x * waves_per_block;
+    const int l = lane_id();
+    uint8_t *base = lds + 1024 + (uint64_t)wib * a.wave_bytes;
+    const InflateLayout L = inflate_layout<kHbm>(a.lds_max_out, a.lds_max_in);
+    InflateWave<kHbm> W;
+    W.sc = reinterpret_cast<InflateScratch *>(base + L.scr);
+    W.crc_tab = crc_tab;
+    // groups of 64 members per wave; this variant's members picked out by ballot
+    for (uint64_t g = wave * 64; g < a.n; g += nwaves * 64) {
+      const uint64_t vl = g + (uint64_t)l;
+      uint32_t my_in = 0, my_cap = 0;
+      if (vl < a.n) {
+          my_in = a.src_len[vl];
+          my_cap = a.dst_cap[vl];
+      }
+      const bool my_fits = my_cap <= a.lds_max_out && my_in <= a.lds_max_in;
+      uint64_t todo = ballot(vl < a.n && (kHbm != my_fits));
+      while (todo) {
+        const int j = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint64_t v = g + (uint64_t)j;
+        const uint64_t in_len = rfl((uint32_t)__shfl(my_in, j));
+        const uint64_t cap = rfl((uint32_t)__shfl(my_cap, j));
+        const uint8_t *src = a.src + a.src_off[v];
+        uint8_t *dst = a.dst + a.dst_off[v];
+        if (in_len == 0) {
+            if (l == 0) {
+                a.rc[v] = PMC_INVALID_INPUT_DEV;
+                a.dst_len[v] = 0;
+            }
+            continue;
+        }
+        if (kHbm) {
+            W.inb = const_cast<uint8_t *>(src);
+            W.out = dst;
+        } else {
+            W.inb = base + L.in;
+            W.out = base + L.out;
+        }
+        int rc = W.run(src, in_len, dst, cap, a.dst_len + v);
+        if (l == 0) {
+            a.rc[v] = rc;
+            if (rc) a.dst_len[v] = 0;
+        }
+      }
+    }
+}
+
+template __global__ void inflate_kernel<false>(InflateArgs);
+template __global__ void inflate_kernel<true>(InflateArgs);
+
+} // namespace pmc

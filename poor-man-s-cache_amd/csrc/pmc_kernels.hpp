@@ -1,0 +1,63 @@
+// pmc_kernels.hpp -- launch-argument structs and sizing shared by the kernels and the
+// host side of the C-ABI (pmc_capi.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pmc {
+
+constexpr int PMC_INVALID_INPUT_DEV = -999;
+constexpr int PMC_Z_DATA_ERROR_DEV = -3;
+constexpr int PMC_Z_BUF_ERROR_DEV = -5;
+constexpr int PMC_E_CAPACITY_DEV = -101;
+
+constexpr uint32_t kSlabSyms = 16384; // per-wave symbol slab (>= 16383 symbols per block)
+
+// Worst case gzip member size (same formula as oracle_gzip_bound): stored fallback adds
+// 5 B per 16383-symbol block; after a window slide fixed/dynamic blocks stay <= 9/8 len.
+__host__ __device__ inline uint64_t gzip_bound(uint64_t len) {
+    return len + (len >> 3) + 6 * (len / 16383 + 1) + 32;
+}
+
+struct DeflateArgs {
+    const uint8_t *src;
+    const uint64_t *src_off;
+    const uint32_t *src_len;
+    uint8_t *dst;
+    const uint64_t *dst_off;
+    const uint32_t *dst_cap;
+    uint32_t *dst_len;
+    int32_t *rc;
+    uint64_t n;
+    uint64_t cap_len;     // working-set capacity (max value length handled)
+    uint64_t lds_max_len; // values <= this go to the LDS kernel, larger to the HBM kernel
+    uint64_t wave_bytes;  // per-wave working set bytes
+    uint32_t *tokens;     // per-wave symbol slabs (kSlabSyms each)
+    uint8_t *scratch;     // per-wave HBM working sets (HBM variant)
+};
+
+struct InflateArgs {
+    const uint8_t *src;
+    const uint64_t *src_off;
+    const uint32_t *src_len;
+    uint8_t *dst;
+    const uint64_t *dst_off;
+    const uint32_t *dst_cap;
+    uint32_t *dst_len;
+    int32_t *rc;
+    uint64_t n;
+    uint64_t lds_max_out; // values whose output fits the LDS image go to the LDS kernel
+    uint64_t lds_max_in;
+    uint64_t wave_bytes;
+    uint8_t *scratch;
+};
+
+uint64_t deflate_wave_bytes(bool hbm, uint64_t n);
+uint64_t inflate_wave_bytes(bool hbm, uint64_t max_out, uint64_t max_in);
+
+template <bool kHbm>
+__global__ void deflate_kernel(DeflateArgs a);
+template <bool kHbm>
+__global__ void inflate_kernel(InflateArgs a);
+
+} // namespace pmc

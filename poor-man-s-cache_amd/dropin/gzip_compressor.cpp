@@ -1,0 +1,47 @@
+// gzip_compressor.cpp -- GzipCompressor over the MI355X codec C-ABI.
+//
+// Same contract as /root/reference/src/compressor/gzip_compressor.cpp:
+//   Compress  (:3-50)   null/empty -> {nullptr, 0, -999}; input length is strlen(input);
+//                       success -> {new[] buffer, size, 0}; failure -> {nullptr, 0, rc}
+//   Decompress(:52-111) null/0 -> {nullptr, -999}; success -> NUL-terminated new[] buffer;
+//                       corrupt -> {nullptr, -3}.  One intentional divergence: a truncated
+//                       stream returns {nullptr, -5} where the reference loops forever
+//                       (SURVEY.md §5).
+// Differences that do not change the contract: the compressed buffer is sized to the
+// gzip bound instead of a >= 16 KiB chunk multiple, and there is no zlib dependency.
+#include "gzip_compressor.hpp"
+
+#include <cstdint>
+
+#include "pmc_codec.h"
+
+CompressResult GzipCompressor::Compress(const char *input) {
+    if (!input || *input == '\0') return {nullptr, 0, INVALID_INPUT};
+    const size_t len = strlen(input);
+    const size_t cap = pmc_gzip_bound(len);
+    char *out = new char[cap];
+    size_t n = 0;
+    int rc = pmc_gzip_compress(pmc_default_ctx(), input, len, out, cap, &n);
+    if (rc != OPERATION_SUCCESS) {
+        delete[] out;
+        return {nullptr, 0, rc};
+    }
+    return {out, n, OPERATION_SUCCESS};
+}
+
+DecompressResult GzipCompressor::Decompress(const char *input, size_t input_size) {
+    if (!input || input_size == 0) return {nullptr, INVALID_INPUT};
+    // ISIZE sizes the output; a lying ISIZE makes the stream fail its length check (-3).
+    // DEFLATE expands at most 1032:1, so a larger ISIZE cannot belong to a valid member.
+    size_t cap = pmc_gzip_isize(input, input_size);
+    if (cap > 1032 * input_size + 64) cap = 1032 * input_size + 64;
+    char *out = new char[cap + 1];
+    size_t n = 0;
+    int rc = pmc_gzip_decompress(pmc_default_ctx(), input, input_size, out, cap, &n);
+    if (rc != OPERATION_SUCCESS) {
+        delete[] out;
+        return {nullptr, rc};
+    }
+    out[n] = '\0';
+    return {out, OPERATION_SUCCESS};
+}

@@ -1,0 +1,237 @@
+"""pmc_codec -- Python host mirror of the MI355X value codec.
+
+Mirrors the reference's codec interface (/root/reference/src/compressor/gzip_compressor.hpp:
+CompressResult / DecompressResult / GzipCompressor::Compress / ::Decompress, codes
+INVALID_INPUT=-999, OPERATION_SUCCESS=0) on top of the C-ABI in include/pmc_codec.h,
+plus the batched device-resident API the GPU hot path is measured through.
+
+The HIP library (libpmc_codec.so, built for gfx950) is REQUIRED: importing works without a
+GPU (so the CPU test suite can check exports), but every compute call raises
+CodecUnavailable when no gfx950 device/context is available.  There is no CPU fallback.
+"""
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpmc_codec.so")
+DROPIN_PATH = os.path.join(HERE, "libgzip_dropin.so")
+
+CHUNK_SIZE = 16384
+INVALID_INPUT = -999
+OPERATION_SUCCESS = 0
+Z_DATA_ERROR = -3
+Z_MEM_ERROR = -4
+Z_BUF_ERROR = -5
+E_NO_DEVICE = -100
+E_CAPACITY = -101
+E_ARG = -102
+
+
+class CodecUnavailable(RuntimeError):
+    pass
+
+
+_lib = None
+
+_c = ctypes
+_p = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+
+# name -> (restype, argtypes) for every function in include/pmc_codec.h
+SIGNATURES = {
+    "pmc_ctx_create": (_c.c_int, [_c.c_int, _c.POINTER(_p)]),
+    "pmc_ctx_destroy": (None, [_p]),
+    "pmc_default_ctx": (_p, []),
+    "pmc_last_error": (_c.c_char_p, []),
+    "pmc_version": (_c.c_char_p, []),
+    "pmc_gzip_bound": (_c.c_size_t, [_c.c_size_t]),
+    "pmc_gzip_compress": (_c.c_int, [_p, _p, _c.c_size_t, _p, _c.c_size_t, _c.POINTER(_c.c_size_t)]),
+    "pmc_gzip_decompress": (_c.c_int, [_p, _p, _c.c_size_t, _p, _c.c_size_t, _c.POINTER(_c.c_size_t)]),
+    "pmc_gzip_isize": (_u32, [_p, _c.c_size_t]),
+    "pmc_gzip_compress_batch": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p, _u32, _p]),
+    "pmc_gzip_decompress_batch": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p, _u32, _p]),
+    "pmc_gzip_isize_batch": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p]),
+    "pmc_gzip_compress_batch_host": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p]),
+    "pmc_gzip_decompress_batch_host": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p]),
+    "pmc_gen_values": (_c.c_int, [_p, _u32, _u64, _c.c_int, _u64, _p, _u32, _u32, _p, _p]),
+    "pmc_fill_layout": (_c.c_int, [_p, _p, _p, _u32, _u64, _u32, _u32, _p]),
+    "pmc_compare_values": (_c.c_int, [_p, _p, _p, _p, _p, _p, _u32, _p, _p]),
+    "pmc_route_keys": (_c.c_int, [_u64, _u32, _u32, _u32, _p, _p]),
+}
+
+
+def lib():
+    """Load libpmc_codec.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise CodecUnavailable(f"{LIB_PATH} missing: run `make -C poor-man-s-cache_amd` "
+                                   "(hipcc --offload-arch=gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().pmc_last_error().decode()
+
+
+def gzip_bound(n: int) -> int:
+    return lib().pmc_gzip_bound(n)
+
+
+def decompress_capacity(member: bytes) -> int:
+    """Output capacity for one gzip member: its ISIZE trailer, clamped to DEFLATE's
+    1032:1 maximum expansion (a larger ISIZE cannot belong to a valid member)."""
+    isz = int.from_bytes(member[-4:], "little") if len(member) >= 18 else 0
+    return min(isz, 1032 * len(member) + 64)
+
+
+class Context:
+    """One device: stream, symbol slabs, HBM working sets, pinned staging."""
+
+    def __init__(self, device: int = 0):
+        self.handle = _p()
+        rc = lib().pmc_ctx_create(device, ctypes.byref(self.handle))
+        if rc != 0:
+            raise CodecUnavailable(f"pmc_ctx_create({device}) = {rc}: {last_error()}")
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            lib().pmc_ctx_destroy(self.handle)
+            self.handle = _p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------- host-resident batches (pinned H2D -> GPU -> D2H) --------------
+    def compress_many(self, values):
+        """values: list of bytes -> list of (rc, gzip bytes)."""
+        return self._host_batch(values, True)
+
+    def decompress_many(self, members, caps=None):
+        """members: list of gzip bytes -> list of (rc, bytes).  caps default: ISIZE."""
+        return self._host_batch(members, False, caps)
+
+    def _host_batch(self, items, compress, caps=None):
+        import numpy as np
+        n = len(items)
+        if n == 0:
+            return []
+        L = lib()
+        src = b"".join(items)
+        src_len = np.array([len(x) for x in items], dtype=np.uint32)
+        src_off = np.zeros(n, dtype=np.uint64)
+        src_off[1:] = np.cumsum(src_len[:-1], dtype=np.uint64)
+        if compress:
+            cap = np.array([gzip_bound(len(x)) for x in items], dtype=np.uint32)
+        elif caps is not None:
+            cap = np.asarray(caps, dtype=np.uint32)
+        else:
+            cap = np.array([decompress_capacity(x) for x in items], dtype=np.uint32)
+        dst_off = np.zeros(n, dtype=np.uint64)
+        dst_off[1:] = np.cumsum(cap[:-1], dtype=np.uint64)
+        dst = ctypes.create_string_buffer(int(cap.sum()) + 1)
+        dst_len = np.zeros(n, dtype=np.uint32)
+        rc = np.zeros(n, dtype=np.int32)
+        fn = L.pmc_gzip_compress_batch_host if compress else L.pmc_gzip_decompress_batch_host
+        r = fn(self.handle, src, src_off.ctypes.data, src_len.ctypes.data, n, dst, dst_off.ctypes.data,
+               cap.ctypes.data, dst_len.ctypes.data, rc.ctypes.data)
+        if r != 0:
+            raise CodecUnavailable(f"batch call failed {r}: {last_error()}")
+        raw = dst.raw
+        return [(int(rc[i]), raw[int(dst_off[i]):int(dst_off[i]) + int(dst_len[i])] if rc[i] == 0 else b"")
+                for i in range(n)]
+
+    # ---------------- device-resident batches (the hot path) ------------------------
+    def compress_device(self, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, max_len, stream=0):
+        """All tensor arguments are torch CUDA tensors (or raw device pointers as int)."""
+        r = lib().pmc_gzip_compress_batch(self.handle, _ptr(src), _ptr(src_off), _ptr(src_len), _n(src_len),
+                                          _ptr(dst), _ptr(dst_off), _ptr(dst_cap), _ptr(dst_len), _ptr(rc),
+                                          max_len, stream)
+        if r != 0:
+            raise CodecUnavailable(f"pmc_gzip_compress_batch = {r}: {last_error()}")
+
+    def decompress_device(self, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, max_len, stream=0):
+        r = lib().pmc_gzip_decompress_batch(self.handle, _ptr(src), _ptr(src_off), _ptr(src_len), _n(src_len),
+                                            _ptr(dst), _ptr(dst_off), _ptr(dst_cap), _ptr(dst_len), _ptr(rc),
+                                            max_len, stream)
+        if r != 0:
+            raise CodecUnavailable(f"pmc_gzip_decompress_batch = {r}: {last_error()}")
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+def _n(t):
+    return t.numel() if hasattr(t, "numel") else int(t)
+
+
+_default: Optional[Context] = None
+
+
+def default_context() -> Context:
+    global _default
+    if _default is None:
+        _default = Context(0)
+    return _default
+
+
+# ------------------------------------------------------------ reference mirror
+@dataclass
+class CompressResult:
+    """gzip_compressor.hpp:16-23"""
+    data: Optional[bytes]
+    size: int
+    operationResult: int
+
+
+@dataclass
+class DecompressResult:
+    """gzip_compressor.hpp:26-31 (data is the NUL-free payload, as a C string would read)"""
+    data: Optional[bytes]
+    operationResult: int
+
+
+class GzipCompressor:
+    """Static-method mirror of the reference class (gzip_compressor.hpp:33-44)."""
+
+    @staticmethod
+    def Compress(input: Optional[bytes]) -> CompressResult:
+        # gzip_compressor.cpp:4,6 -- null/empty rejected; the value is a C string (strlen)
+        if input is None:
+            return CompressResult(None, 0, INVALID_INPUT)
+        s = bytes(input).split(b"\0", 1)[0]
+        if not s:
+            return CompressResult(None, 0, INVALID_INPUT)
+        rc, out = default_context().compress_many([s])[0]
+        if rc != 0:
+            return CompressResult(None, 0, rc)
+        return CompressResult(out, len(out), OPERATION_SUCCESS)
+
+    @staticmethod
+    def Decompress(input: Optional[bytes], input_size: int) -> DecompressResult:
+        # gzip_compressor.cpp:53 -- null or size 0 rejected
+        if input is None or input_size == 0:
+            return DecompressResult(None, INVALID_INPUT)
+        data = bytes(input[:input_size])
+        rc, out = default_context().decompress_many([data])[0]
+        if rc != 0:
+            return DecompressResult(None, rc)
+        return DecompressResult(out, OPERATION_SUCCESS)

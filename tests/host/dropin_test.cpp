@@ -1,0 +1,118 @@
+// dropin_test.cpp -- the reference's gzip_compressor_test.cpp (:6-95) and the codec half of
+// KeyValueStoreTest.LargeJSONFiles (kvs_test.cpp:36-65), re-expressed without gtest, run
+// against the drop-in GzipCompressor (poor-man-s-cache_amd/dropin) on the GPU.
+// Additionally every compressed buffer is compared with the golden bytes passed on argv.
+// usage: dropin_test <tests/golden/data dir> <golden gz dir>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <dirent.h>
+#include <string>
+#include <vector>
+
+#include "gzip_compressor.hpp"
+
+static int failures = 0;
+#define EXPECT(c)                                                            \
+    do {                                                                     \
+        if (!(c)) {                                                          \
+            fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c);     \
+            failures++;                                                      \
+        }                                                                    \
+    } while (0)
+
+static std::string slurp(const std::string &p) {
+    FILE *f = fopen(p.c_str(), "rb");
+    if (!f) return {};
+    std::string s;
+    char buf[65536];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, n);
+    fclose(f);
+    return s;
+}
+
+int main(int argc, char **argv) {
+    // CompressDecompress (:6-22)
+    {
+        auto input = "Hello, Gzip!";
+        auto c = GzipCompressor::Compress(input);
+        EXPECT(c.data != nullptr && c.size != 0 && c.operationResult == OPERATION_SUCCESS);
+        auto d = GzipCompressor::Decompress(c.data, c.size);
+        EXPECT(d.data != nullptr && d.operationResult == OPERATION_SUCCESS);
+        EXPECT(d.data && strcmp(d.data, input) == 0);
+        delete[] c.data;
+        delete[] d.data;
+    }
+    // CompressEmptyString (:25-36)
+    {
+        auto c = GzipCompressor::Compress("");
+        EXPECT(c.data == nullptr && c.size == 0 && c.operationResult == INVALID_INPUT);
+        auto d = GzipCompressor::Decompress(c.data, c.size);
+        EXPECT(d.data == nullptr && d.operationResult == INVALID_INPUT);
+    }
+    // CompressNullInput (:39-48)
+    {
+        auto c = GzipCompressor::Compress(nullptr);
+        EXPECT(c.data == nullptr && c.size == 0 && c.operationResult == INVALID_INPUT);
+        auto d = GzipCompressor::Decompress(c.data, c.size);
+        EXPECT(d.data == nullptr && d.operationResult == INVALID_INPUT);
+    }
+    // CompressDecompressLongString (:51-71)
+    {
+        auto input = "This is a long test string. "
+                     "It should be compressed and decompressed properly. "
+                     "We are testing to see if gzip can handle long input.";
+        auto c = GzipCompressor::Compress(input);
+        EXPECT(c.data != nullptr && c.operationResult == OPERATION_SUCCESS);
+        EXPECT(c.size < strlen(input));
+        auto d = GzipCompressor::Decompress(c.data, c.size);
+        EXPECT(d.data && strcmp(d.data, input) == 0);
+        delete[] c.data;
+        delete[] d.data;
+    }
+    // CompressionReducesSize (:74-86)
+    {
+        auto input = "AAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA";
+        auto c = GzipCompressor::Compress(input);
+        EXPECT(c.data != nullptr && c.operationResult == OPERATION_SUCCESS && c.size < strlen(input));
+        delete[] c.data;
+    }
+    // DecompressInvalidData (:89-95)
+    {
+        auto bad = "Not a gzip string";
+        auto d = GzipCompressor::Decompress(bad, strlen(bad));
+        EXPECT(d.data == nullptr && d.operationResult < OPERATION_SUCCESS);
+    }
+    // Truncated stream: documented divergence (-5 instead of the reference's hang)
+    {
+        auto c = GzipCompressor::Compress("truncate me truncate me truncate me truncate me");
+        auto d = GzipCompressor::Decompress(c.data, c.size - 9);
+        EXPECT(d.data == nullptr && d.operationResult == -5);
+        delete[] c.data;
+    }
+    // LargeJSONFiles codec path (kvs_test.cpp:36-65): set = Compress, get = Decompress
+    if (argc >= 3) {
+        std::string dir = argv[1], gdir = argv[2];
+        DIR *dp = opendir(dir.c_str());
+        int files = 0;
+        for (dirent *e; dp && (e = readdir(dp));) {
+            std::string name = e->d_name;
+            if (name.size() < 5 || name.substr(name.size() - 5) != ".json") continue;
+            std::string content = slurp(dir + "/" + name);
+            std::string want = slurp(gdir + "/" + name + ".gz");
+            auto c = GzipCompressor::Compress(content.c_str());
+            EXPECT(c.operationResult == OPERATION_SUCCESS);
+            EXPECT(c.size == want.size() && memcmp(c.data, want.data(), c.size) == 0);
+            auto d = GzipCompressor::Decompress(c.data, c.size);
+            EXPECT(d.data && strcmp(d.data, content.c_str()) == 0);
+            delete[] c.data;
+            delete[] d.data;
+            files++;
+        }
+        if (dp) closedir(dp);
+        EXPECT(files == 6);
+    }
+    printf("dropin_test: %d failure(s)\n", failures);
+    return failures ? 1 : 0;
+}

@@ -1,0 +1,268 @@
+"""GPU parity: the HIP codec (through the C-ABI) vs the reference's goldens and the oracle.
+
+Bar: bit-exact bytes for every compressed value, exact bytes back for every decompressed
+value, the reference's verdict for every corrupt/truncated member.
+"""
+import hashlib
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch  # noqa: F401  (device memory / streams)
+    import pmc_codec
+    c = pmc_codec.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def D():
+    from pmc_codec import device
+    return device
+
+
+def sync():
+    import torch
+    torch.cuda.synchronize()
+
+
+def test_library_is_the_hip_one(ctx):
+    import pmc_codec
+    assert b"gfx950" in pmc_codec.lib().pmc_version()
+
+
+def test_compress_all_golden_vectors(ctx, D, golden):
+    """755 vectors, 1 B .. 82 KB in ONE ragged batch: LDS and HBM kernel variants."""
+    pairs = golden.pairs()
+    b = D.pack([r for r, _ in pairs])
+    out, rc = D.compress(ctx, b)
+    sync()
+    rc = rc.cpu().numpy()
+    got = out.host_items()
+    bad = [k for k, (r, g) in enumerate(pairs) if rc[k] != 0 or got[k] != g]
+    assert not bad, f"{len(bad)} vectors differ; first {bad[:8]} sizes {[len(pairs[k][0]) for k in bad[:8]]}"
+
+
+def test_decompress_all_golden_vectors(ctx, D, golden):
+    pairs = golden.pairs()
+    b = D.pack([g for _, g in pairs])
+    out, rc = D.decompress(ctx, b)
+    sync()
+    rc = rc.cpu().numpy()
+    got = out.host_items()
+    bad = [k for k, (r, g) in enumerate(pairs) if rc[k] != 0 or got[k] != r]
+    assert not bad, f"{len(bad)} vectors differ; first {bad[:8]}"
+
+
+def test_decompress_error_verdicts(ctx, D, golden):
+    errs = golden.index["decompress_errors"]
+    b = D.pack([bytes.fromhex(e["hex"]) for e in errs])
+    out, rc = D.decompress(ctx, b)
+    sync()
+    rc = rc.cpu().numpy()
+    for k, e in enumerate(errs):
+        assert rc[k] == e["expect_rc"], (e["name"], rc[k])
+
+
+def test_corruption_fuzz_matches_oracle(ctx, D):
+    """bit flips and truncations: same verdict as the oracle (zlib's rules)."""
+    from oracle import pyoracle as O
+    rng = np.random.default_rng(11)
+    base = [O.compress(bytes(rng.integers(97, 103, n, dtype=np.uint8))) for n in (40, 300, 2000)]
+    base.append(O.compress(bytes(rng.integers(0, 256, 700, dtype=np.uint8))))
+    vecs = []
+    for z in base:
+        for _ in range(150):
+            t = bytearray(z)
+            t[rng.integers(len(t))] ^= 1 << int(rng.integers(8))
+            vecs.append(bytes(t))
+        for _ in range(50):
+            vecs.append(z[:int(rng.integers(1, len(z)))])
+    b = D.pack(vecs)
+    import pmc_codec
+    caps = [pmc_codec.decompress_capacity(v) for v in vecs]
+    out, rc = D.decompress(ctx, b, caps)
+    sync()
+    rc = rc.cpu().numpy()
+    got = out.host_items()
+    for k, v in enumerate(vecs):
+        erc, eout = O.decompress(v, cap=max(caps[k], 1))
+        assert rc[k] == erc, (k, rc[k], erc)
+        if erc == 0:
+            assert got[k] == eout
+
+
+def test_digest_sets_generated_on_device(ctx, D, golden):
+    """Values generated on the GPU (SURVEY §8d generator) -> compressed -> SHA-256 of the
+    concatenated members equals the digest of the reference's output."""
+    import torch
+    import pmc_codec
+    L = pmc_codec.lib()
+    corpus = torch.frombuffer(bytearray(golden.corpus), dtype=torch.uint8).cuda()
+    for d in golden.index["digests"]:
+        n, vlen = d["n"], d["vlen"]
+        data = torch.empty(n * vlen + 16, dtype=torch.uint8, device="cuda")
+        assert L.pmc_gen_values(corpus.data_ptr(), len(golden.corpus), d["seed"], d["kind"], 0, None, n, vlen,
+                                data.data_ptr(), D.stream_handle()) == 0
+        off = torch.arange(n, dtype=torch.int64, device="cuda") * vlen
+        lens = torch.full((n,), vlen, dtype=torch.int32, device="cuda")
+        out, rc = D.compress(ctx, D.Batch(data, off, lens, n, vlen))
+        sync()
+        assert int((rc != 0).sum()) == 0
+        items = out.host_items()
+        h = hashlib.sha256(b"".join(items)).hexdigest()
+        sizes = np.asarray([len(x) for x in items], np.uint32)
+        assert h == d["sha256"], d
+        assert hashlib.sha256(sizes.tobytes()).hexdigest() == d["sizes_sha256"]
+
+
+def test_ragged_edge_sizes_vs_oracle(ctx, D, golden):
+    from oracle import pyoracle as O
+    rng = np.random.default_rng(7)
+    sizes = [1, 2, 3, 4, 29, 30, 63, 64, 65, 257, 258, 259, 260, 1023, 1024, 1025, 4096, 13000, 16383,
+             16384, 16385, 32505, 32506, 32507, 32768, 40000, 65274, 65275, 65536, 70000, 131072, 150001]
+    vals = []
+    for s in sizes:
+        o = int(rng.integers(0, max(1, len(golden.corpus) - s)))
+        vals.append((golden.corpus * 2)[o:o + s])
+        vals.append(bytes(rng.integers(0, 4, s, dtype=np.uint8)))           # binary, NULs
+        vals.append(bytes(rng.integers(0, 256, s, dtype=np.uint8)))         # stored blocks
+        vals.append(b"ab" * (s // 2) + b"a" * (s % 2))                      # long matches
+    vals.insert(5, b"")  # invalid input inside a batch
+    b = D.pack(vals)
+    out, rc = D.compress(ctx, b)
+    sync()
+    rc = rc.cpu().numpy()
+    got = out.host_items()
+    for k, v in enumerate(vals):
+        if len(v) == 0:
+            assert rc[k] == -999
+            continue
+        assert rc[k] == 0, (k, len(v), rc[k])
+        assert got[k] == O.compress(v), (k, len(v))
+    # and back
+    ok = [k for k, v in enumerate(vals) if len(v)]
+    b2 = D.pack([got[k] for k in ok])
+    out2, rc2 = D.decompress(ctx, b2, [len(vals[k]) for k in ok])
+    sync()
+    assert int((rc2 != 0).sum()) == 0
+    back = out2.host_items()
+    for j, k in enumerate(ok):
+        assert back[j] == vals[k]
+
+
+@pytest.mark.parametrize("vlen,kind,n", [(256, 0, 200_000), (1024, 0, 200_000), (4096, 0, 40_000),
+                                         (1024, 1, 50_000)])
+def test_roundtrip_at_scale(ctx, D, golden, vlen, kind, n):
+    """Size-independent properties at scale: every value round-trips (compared on the GPU),
+    every rc is 0, and a random sample is byte-identical to the oracle."""
+    import torch
+    import pmc_codec
+    from oracle import pyoracle as O
+    L = pmc_codec.lib()
+    seed = 0x5EED if kind == 0 else 0xA1B2
+    corpus = torch.frombuffer(bytearray(golden.corpus), dtype=torch.uint8).cuda()
+    data = torch.empty(n * vlen + 16, dtype=torch.uint8, device="cuda")
+    assert L.pmc_gen_values(corpus.data_ptr(), len(golden.corpus), seed, kind, 1000, None, n, vlen, data.data_ptr(),
+                            D.stream_handle()) == 0
+    off = torch.arange(n, dtype=torch.int64, device="cuda") * vlen
+    lens = torch.full((n,), vlen, dtype=torch.int32, device="cuda")
+    src = D.Batch(data, off, lens, n, vlen)
+    comp, rc = D.compress(ctx, src)
+    caps = torch.full((n,), vlen, dtype=torch.int32, device="cuda")
+    dst = torch.empty(n * vlen + 16, dtype=torch.uint8, device="cuda")
+    dlen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    rc2 = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ctx.decompress_device(comp.data, comp.off, comp.len, dst, off, caps, dlen, rc2, vlen, D.stream_handle())
+    mism = torch.zeros(1, dtype=torch.int32, device="cuda")
+    assert L.pmc_compare_values(data.data_ptr(), off.data_ptr(), dst.data_ptr(), off.data_ptr(),
+                                lens.data_ptr(), dlen.data_ptr(), n, mism.data_ptr(), D.stream_handle()) == 0
+    sync()
+    assert int((rc != 0).sum()) == 0 and int((rc2 != 0).sum()) == 0
+    assert int(mism.item()) == 0
+    rng = np.random.default_rng(vlen + kind)
+    host_vals = O.gen_values(golden.corpus, seed, kind, 1000, n, vlen)
+    clen = comp.len.cpu().numpy()
+    coff = comp.off.cpu().numpy()
+    for i in rng.choice(n, 300, replace=False):
+        got = comp.data[int(coff[i]):int(coff[i]) + int(clen[i])].cpu().numpy().tobytes()
+        assert got == O.compress(host_vals[i].tobytes()), i
+
+
+def test_python_mirror_reference_unit_cases(ctx):
+    """gzip_compressor_test.cpp:6-95 through the Python mirror of GzipCompressor."""
+    from pmc_codec import GzipCompressor, INVALID_INPUT, OPERATION_SUCCESS
+    c = GzipCompressor.Compress(b"Hello, Gzip!")
+    assert c.data and c.size and c.operationResult == OPERATION_SUCCESS
+    d = GzipCompressor.Decompress(c.data, c.size)
+    assert d.operationResult == OPERATION_SUCCESS and d.data == b"Hello, Gzip!"
+    e = GzipCompressor.Compress(b"")
+    assert e.data is None and e.size == 0 and e.operationResult == INVALID_INPUT
+    assert GzipCompressor.Decompress(None, 0).operationResult == INVALID_INPUT
+    assert GzipCompressor.Compress(None).operationResult == INVALID_INPUT
+    s = (b"This is a long test string. It should be compressed and decompressed properly. "
+         b"We are testing to see if gzip can handle long input.")
+    c = GzipCompressor.Compress(s)
+    assert c.size < len(s) and GzipCompressor.Decompress(c.data, c.size).data == s
+    assert GzipCompressor.Compress(b"A" * 50).size < 50
+    bad = GzipCompressor.Decompress(b"Not a gzip string", 17)
+    assert bad.data is None and bad.operationResult < 0
+
+
+def test_cpp_dropin_links_and_passes(ctx, golden):
+    """The drop-in GzipCompressor (C++) runs the reference's own unit cases and the
+    LargeJSONFiles codec path, with bytes equal to the reference's."""
+    import pmc_codec
+    d = tempfile.mkdtemp(prefix="pmc_dropin_")
+    for k, (name, data) in enumerate(golden.data_files):
+        r, g = golden.pair(k)
+        assert r == data
+        with open(os.path.join(d, name + ".gz"), "wb") as f:
+            f.write(g)
+    exe = os.path.join(d, "dropin_test")
+    pkg = os.path.dirname(pmc_codec.LIB_PATH)
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "poor-man-s-cache_amd", "dropin"),
+                           "-o", exe, os.path.join(ROOT, "tests", "host", "dropin_test.cpp"),
+                           "-L", pkg, "-lgzip_dropin", "-lpmc_codec", "-Wl,-rpath," + pkg])
+    r = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "data"), d], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_route_keys_vs_oracle(ctx, D):
+    import ctypes
+    import torch
+    import pmc_codec
+    from oracle import pyoracle as O
+    L = O.lib()
+    L.oracle_murmur3_x64_128_h1.restype = ctypes.c_uint64
+    L.oracle_murmur3_x64_128_h1.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32]
+    n = 5000
+    gpu = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    assert pmc_codec.lib().pmc_route_keys(0, n, 128, 8, gpu.data_ptr(), D.stream_handle()) == 0
+    sync()
+    g = gpu.cpu().numpy()
+    for i in range(n):
+        k = b"key%d" % i
+        assert g[i] == (L.oracle_murmur3_x64_128_h1(k, len(k), 0) % 128) % 8, i
+
+
+def test_host_batch_api(ctx, golden):
+    from oracle import pyoracle as O
+    vals = [r for r, _ in golden.pairs()[:40] if r]
+    out = ctx.compress_many(vals)
+    for (rc, gz), v in zip(out, vals):
+        assert rc == 0 and gz == O.compress(v)
+    back = ctx.decompress_many([gz for _, gz in out])
+    for (rc, r), v in zip(back, vals):
+        assert rc == 0 and r == v

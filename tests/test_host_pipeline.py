@@ -1,0 +1,32 @@
+"""CPU: the device Huffman / emit code (pmc_trees.hpp) compiled with g++ and driven the
+way the kernel drives it (tests/host/host_pipeline.cpp) reproduces every golden vector."""
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def host_bin():
+    d = tempfile.mkdtemp(prefix="pmc_host_")
+    exe = os.path.join(d, "host_pipeline")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-o", exe,
+                           os.path.join(HERE, "host", "host_pipeline.cpp")])
+    return exe, d
+
+
+def test_host_pipeline_matches_goldens(golden, host_bin):
+    exe, d = host_bin
+    src, dst = os.path.join(d, "in"), os.path.join(d, "out")
+    bad = []
+    for k, (r, g) in enumerate(golden.pairs()):
+        with open(src, "wb") as f:
+            f.write(r)
+        subprocess.check_call([exe, src, dst])
+        with open(dst, "rb") as f:
+            if f.read() != g:
+                bad.append(k)
+    assert not bad, bad[:10]
