@@ -1,0 +1,274 @@
+#!/usr/bin/env python
+"""bench.py -- device-resident gzip-9 compress+decompress throughput on MI355X.
+
+Metric (BASELINE.json): "device-resident value compress+decompress GiB/s at 1/2/4/8 MI355X".
+One step = compress every value of this rank's batch, then decompress every member back,
+inputs already resident in HBM.  value = (all ranks' uncompressed bytes) / (max over ranks
+of the step time), in GiB/s.  Workload (north star / BASELINE configs[3] per GPU):
+10M x 1 KiB JSON-slice values per GPU, routed to GPUs by MurmurHash3("key"+i) % 128 % N
+(NUM_SHARDS=128 as deployed) -- weak scaling, no collective on the data path.
+
+Single GPU:  python bench.py [--steps K --warmup W]
+Multi GPU :  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "poor-man-s-cache_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "device-resident value compress+decompress GiB/s at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+META_BYTES = 12        # +12 B offset/len per value per direction
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=10_000_000, help="values per GPU")
+    ap.add_argument("--vlen", type=int, default=1024)
+    ap.add_argument("--kind", type=int, default=0, help="0 JSON slices, 1 random alnum")
+    ap.add_argument("--cpu-sample", type=int, default=300_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--h2h", action="store_true", help="also time pinned H2D+kernel+D2H (host-to-host)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (from scripts/pmc_traffic.py), if present")
+    return ap.parse_args()
+
+
+def load_corpus():
+    d = os.path.join(ROOT, "tests", "golden", "data")
+    return b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)) if f.endswith(".json"))
+
+
+def cpu_baseline(corpus, args, index0):
+    """The reference GzipCompressor timed on the host cores (oracle/_ref), or the oracle
+    port if the reference build is absent.  Bounded sample of the same workload."""
+    from oracle import pyoracle as O
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(16, cores))  # the box's CPU share for one GPU
+    seed = 0x5EED if args.kind == 0 else 0xA1B2
+    n = args.cpu_sample
+    vals = O.gen_values(corpus, seed, args.kind, index0, n, args.vlen)
+    if O.ref_available():
+        r = O.ref_bench(vals, cores)
+        assert r["bad"] == 0
+        t = r["t_compress"] + r["t_decompress"]
+        kind, zv = "reference", O.ref().ref_zlib_version().decode()
+    else:
+        import time as _t
+        n = min(n, 20_000)
+        t0 = _t.perf_counter()
+        gz = [O.compress(vals[k].tobytes()) for k in range(n)]
+        t1 = _t.perf_counter()
+        for g in gz:
+            O.decompress(g)
+        t = _t.perf_counter() - t0
+        cores, kind, zv = 1, "port", "oracle restatement of zlib 1.2.11"
+        r = {"t_compress": t1 - t0, "t_decompress": t - (t1 - t0)}
+    gib = n * args.vlen / 2 ** 30
+    cpu = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"value": gib / t, "unit": "GiB/s", "cores": cores, "kind": kind,
+            "sample": f"{n} x {args.vlen} B values of the same workload (indices {index0}..{index0 + n - 1}), "
+                      f"one GzipCompressor::Compress then Decompress per value, {cores} std::threads",
+            "compress_gib_s": gib / r["t_compress"], "decompress_gib_s": gib / r["t_decompress"],
+            "cpu": cpu, "zlib": zv}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import pmc_codec
+    from pmc_codec import device as D
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+    L = pmc_codec.lib()
+    corpus_b = load_corpus()
+    n, vlen = args.n, args.vlen
+    seed = 0x5EED if args.kind == 0 else 0xA1B2
+
+    # ---- CPU baseline first (host idle), rank 0 at N=1 only ------------------------------
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(corpus_b, args, 0)
+
+    ctx = pmc_codec.Context(local)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    # ---- this rank's keys: route "key"+i to GPUs, take the first n routed here -----------
+    if world > 1:
+        span = int(n * world * 1.05) + 4096
+        route = torch.empty(span, dtype=torch.uint8, device=dev)
+        assert L.pmc_route_keys(0, span, 128, world, route.data_ptr(), sh) == 0
+        index = torch.nonzero(route == rank).flatten()[:n].to(torch.int64).contiguous()
+        assert index.numel() == n
+        del route
+        idx_ptr = index.data_ptr()
+    else:
+        index, idx_ptr = None, None
+    corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).to(dev)
+    src = torch.empty(n * vlen + 16, dtype=torch.uint8, device=dev)
+    assert L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), seed, args.kind, 0, idx_ptr, n, vlen,
+                            src.data_ptr(), sh) == 0
+    off = torch.arange(n, dtype=torch.int64, device=dev) * vlen
+    lens = torch.full((n,), vlen, dtype=torch.int32, device=dev)
+    cap = pmc_codec.gzip_bound(vlen)
+    cstride = (cap + 15) // 16 * 16
+    comp = torch.empty(n * cstride + 16, dtype=torch.uint8, device=dev)
+    coff = torch.arange(n, dtype=torch.int64, device=dev) * cstride
+    ccap = torch.full((n,), cap, dtype=torch.int32, device=dev)
+    clen = torch.zeros(n, dtype=torch.int32, device=dev)
+    crc = torch.zeros(n, dtype=torch.int32, device=dev)
+    back = torch.empty(n * vlen + 16, dtype=torch.uint8, device=dev)
+    blen = torch.zeros(n, dtype=torch.int32, device=dev)
+    brc = torch.zeros(n, dtype=torch.int32, device=dev)
+    del index
+
+    def step(evs=None):
+        if evs:
+            evs[0].record(stream)
+        ctx.compress_device(src, off, lens, comp, coff, ccap, clen, crc, vlen, sh)
+        if evs:
+            evs[1].record(stream)
+        ctx.decompress_device(comp, coff, clen, back, off, lens, blen, brc, vlen, sh)
+        if evs:
+            evs[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    tc = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps / 1e3  # s per compress launch set
+    td = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps / 1e3
+
+    # ---- verification of the last step (device-side compare, all values) ----------------
+    mism = torch.zeros(1, dtype=torch.int32, device=dev)
+    assert L.pmc_compare_values(src.data_ptr(), off.data_ptr(), back.data_ptr(), off.data_ptr(), lens.data_ptr(),
+                                blen.data_ptr(), n, mism.data_ptr(), sh) == 0
+    torch.cuda.synchronize()
+    bad = int(mism.item()) + int((crc != 0).sum().item()) + int((brc != 0).sum().item())
+    comp_bytes = int(clen.to(torch.int64).sum().item())
+
+    t_step = torch.tensor([wall / args.steps, tc, td], dtype=torch.float64, device=dev)
+    agg = torch.tensor([float(n * vlen), float(comp_bytes), float(bad)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_step, op=dist.ReduceOp.MAX)
+        dist.all_reduce(agg, op=dist.ReduceOp.SUM)
+    t_step_s, tc_max, td_max = (float(x) for x in t_step.tolist())
+    total_bytes, total_comp, total_bad = (float(x) for x in agg.tolist())
+
+    h2h = None
+    if args.h2h and world == 1:
+        h2h = host_to_host(ctx, src, off, lens, comp, coff, ccap, clen, crc, back, blen, brc, n, vlen, cstride,
+                           stream)
+
+    if rank == 0:
+        gib = total_bytes / 2 ** 30
+        # roofline of the dominant kernel (deflate, LDS variant): algorithmic bytes per launch
+        alg_c = n * (vlen + META_BYTES) + comp_bytes
+        alg_d = comp_bytes + n * (vlen + META_BYTES)
+        traffic = None
+        if os.path.exists(args.traffic):
+            try:
+                with open(args.traffic) as f:
+                    tj = json.load(f)
+                if tj.get("n") == n and tj.get("vlen") == vlen and tj.get("kind") == args.kind:
+                    traffic = tj.get("deflate_hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        achieved = alg_c / tc / 1e9
+        out = {
+            "metric": METRIC, "value": gib / t_step_s, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": t_step_s * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: JSON slices of the reference's tests/data corpus (SURVEY.md §8d generator, "
+                    f"seed {seed:#x})" if args.kind == 0 else "synthetic: random [A-Za-z0-9]",
+            "config": {"workload": f"{n} x {vlen} B values per GPU ({'JSON-slice' if args.kind == 0 else 'alnum'}), "
+                                   "batched gzip level-9 compress + decompress, device-resident, zlib-bit-exact",
+                       "values_per_gpu": n, "value_bytes": vlen, "total_values": n * world,
+                       "partition": "MurmurHash3_x64_128('key'+i)[0] % 128 % n_gpus (NUM_SHARDS=128)",
+                       "parallelism": f"shard-partitioned x{world}, no collective"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "pmc::deflate_kernel<false>",
+                         "alg_bytes_per_launch": alg_c, "avg_launch_ms": tc * 1e3},
+            "cpu_baseline": cpu,
+            "compress_gib_s": gib / world / tc_max, "decompress_gib_s": gib / world / td_max,
+            "decompress_roofline_frac": alg_d / td / 1e9 / HBM_PEAK_GBS,
+            "ratio": total_comp / total_bytes, "verified_values": int(total_bytes // vlen),
+            "mismatches": int(total_bad),
+        }
+        if h2h:
+            out["host_to_host"] = h2h
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def host_to_host(ctx, src, off, lens, comp, coff, ccap, clen, crc, back, blen, brc, n, vlen, cstride, stream):
+    """PCIe-inclusive rates: pinned host buffers -> H2D -> kernel -> D2H."""
+    import torch
+    sh = stream.cuda_stream
+    h_src = torch.empty(src.numel(), dtype=torch.uint8, pin_memory=True)
+    h_comp = torch.empty(comp.numel(), dtype=torch.uint8, pin_memory=True)
+    h_back = torch.empty(back.numel(), dtype=torch.uint8, pin_memory=True)
+    h_src.copy_(src)
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    e[0].record(stream)
+    src.copy_(h_src, non_blocking=True)
+    ctx.compress_device(src, off, lens, comp, coff, ccap, clen, crc, vlen, sh)
+    h_comp.copy_(comp, non_blocking=True)
+    e[1].record(stream)
+    comp.copy_(h_comp, non_blocking=True)
+    ctx.decompress_device(comp, coff, clen, back, off, lens, blen, brc, vlen, sh)
+    h_back.copy_(back, non_blocking=True)
+    e[2].record(stream)
+    torch.cuda.synchronize()
+    tc = e[0].elapsed_time(e[1]) / 1e3
+    td = e[1].elapsed_time(e[2]) / 1e3
+    gib = n * vlen / 2 ** 30
+    return {"compress_gib_s": gib / tc, "decompress_gib_s": gib / td, "roundtrip_gib_s": gib / (tc + td),
+            "note": "whole batch staged: pinned H2D of inputs, kernel, D2H of fixed-stride output slots"}
+
+
+if __name__ == "__main__":
+    main()
