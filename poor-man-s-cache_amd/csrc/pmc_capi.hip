@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -145,7 +146,9 @@ struct pmc_ctx {
     int cus = 0;
     hipStream_t stream = nullptr;
     DevBuf tokens, dscratch;     // deflate symbol slabs / HBM working sets
+    DevBuf fbscratch;            // per-wave Trees for the small kernel's serial fallback
     DevBuf staging;              // device side of host-API calls
+    uint64_t *dbg = nullptr;     // diagnostic stamp sums (PMC_STAMPS builds)
     HostBuf pinned;              // host side of host-API calls
 };
 
@@ -171,6 +174,17 @@ uint64_t deflate_lds_limit() {
     while (lo < hi) {
         uint64_t mid = (lo + hi + 1) / 2;
         if (deflate_wave_bytes(false, mid) + kCrcTabBytes <= kLdsPerCu) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// values up to this length take the single-block small kernel (pmc_deflate_small.hip)
+uint64_t deflate_small_limit() {
+    uint64_t lo = 64, hi = 16382;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi + 1) / 2;
+        if (deflate_small_wave_bytes(mid) + kCrcTabBytes <= kLdsPerCu) lo = mid;
         else hi = mid - 1;
     }
     return lo;
@@ -215,6 +229,8 @@ PMC_API int pmc_ctx_create(int device, pmc_ctx **out) {
     // the LDS-resident kernels may use the whole 160 KiB of a CU
     HIP_TRY(hipFuncSetAttribute((const void *)deflate_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kLdsPerCu));
+    HIP_TRY(hipFuncSetAttribute((const void *)deflate_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)inflate_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)inflate_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -236,6 +252,7 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     c->tokens.release();
     c->dscratch.release();
+    c->fbscratch.release();
     c->staging.release();
     c->pinned.release();
     (void)hipStreamDestroy(c->stream);
@@ -264,44 +281,59 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
     hipStream_t st = (hipStream_t)stream;
-    DeflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, nullptr};
-    const uint64_t lim = deflate_lds_limit();
-    a.lds_max_len = std::min<uint64_t>(lim, std::max<uint64_t>(max_len, 1));
-    // ---- LDS kernel (values <= lds_max_len) ----
-    {
-        uint64_t cap = (a.lds_max_len + 63) & ~(uint64_t)63;
-        if (cap > lim) cap = lim;
-        a.cap_len = cap;
-        uint64_t wb = deflate_wave_bytes(false, cap);
-        Launch L = plan_lds(ctx, (const void *)deflate_kernel<false>, wb, n);
-        a.wave_bytes = wb;
-        uint64_t waves = (uint64_t)L.blocks * L.wpb;
-        int r = ctx->tokens.ensure(waves * kSlabSyms * sizeof(uint32_t));
-        if (r) return r;
-        a.tokens = (uint32_t *)ctx->tokens.p;
-        hipLaunchKernelGGL(deflate_kernel<false>, dim3(L.blocks), dim3(64 * L.wpb), L.lds, st, a);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) {
-            set_err("deflate_kernel<lds>", e);
-            return PMC_E_NO_DEVICE;
-        }
+    DeflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, nullptr,
+                  ctx->dbg};
+    // Values <= small_lim: single-block LDS kernel (pmc_deflate_small.hip).  Larger values:
+    // the general kernel with its working set in HBM (pmc_deflate.hip).  PMC_DEFLATE_V1=1
+    // routes everything through the general kernels (A/B and safety net).
+    static const bool force_v1 = getenv("PMC_DEFLATE_V1") && atoi(getenv("PMC_DEFLATE_V1"));
+    const uint64_t small_lim = force_v1 ? 0 : deflate_small_limit();
+    const uint64_t v1_lim = deflate_lds_limit();
+    const uint64_t lds_cut = force_v1 ? std::min<uint64_t>(v1_lim, std::max<uint64_t>(max_len, 1))
+                                      : std::min<uint64_t>(small_lim, std::max<uint64_t>(max_len, 1));
+    Launch Ls{};
+    uint64_t small_waves = 0, hbm_waves = 0, hbm_wb = 0;
+    const void *lds_kernel = force_v1 ? (const void *)deflate_kernel<false> : (const void *)deflate_small_kernel;
+    uint64_t cap = (lds_cut + 63) & ~(uint64_t)63;
+    cap = std::min<uint64_t>(cap, force_v1 ? v1_lim : small_lim);
+    const uint64_t lds_wb = force_v1 ? deflate_wave_bytes(false, cap) : deflate_small_wave_bytes(cap);
+    Ls = plan_lds(ctx, lds_kernel, lds_wb, n);
+    small_waves = (uint64_t)Ls.blocks * Ls.wpb;
+    if (max_len > lds_cut) {
+        hbm_wb = deflate_wave_bytes(true, max_len);
+        hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 2,
+                                                             (8ull << 30) / std::max<uint64_t>(hbm_wb, 1)));
+        hbm_waves = std::min<uint64_t>(hbm_waves, n);
     }
-    // ---- HBM kernel (values > lds_max_len) ----
-    if (max_len > a.lds_max_len) {
+    // size every per-wave buffer before the first launch (no reallocation under a kernel)
+    int r = ctx->tokens.ensure(std::max(small_waves, hbm_waves) * kSlabSyms * sizeof(uint32_t));
+    if (r) return r;
+    r = ctx->fbscratch.ensure(small_waves * sizeof(Trees));
+    if (r) return r;
+    if (hbm_waves) {
+        r = ctx->dscratch.ensure(hbm_waves * hbm_wb);
+        if (r) return r;
+    }
+    a.tokens = (uint32_t *)ctx->tokens.p;
+    // ---- LDS kernel (values <= lds_cut) ----
+    a.lds_max_len = lds_cut;
+    a.cap_len = cap;
+    a.wave_bytes = lds_wb;
+    a.scratch = (uint8_t *)ctx->fbscratch.p;
+    if (force_v1) hipLaunchKernelGGL(deflate_kernel<false>, dim3(Ls.blocks), dim3(64 * Ls.wpb), Ls.lds, st, a);
+    else hipLaunchKernelGGL(deflate_small_kernel, dim3(Ls.blocks), dim3(64 * Ls.wpb), Ls.lds, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_err("deflate_kernel<lds>", e);
+        return PMC_E_NO_DEVICE;
+    }
+    // ---- HBM kernel (values > lds_cut) ----
+    if (hbm_waves) {
         a.cap_len = max_len;
-        uint64_t wb = deflate_wave_bytes(true, max_len);
-        uint64_t waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 2,
-                                                                  (8ull << 30) / std::max<uint64_t>(wb, 1)));
-        waves = std::min<uint64_t>(waves, n);
-        int r = ctx->dscratch.ensure(waves * wb);
-        if (r) return r;
-        r = ctx->tokens.ensure(std::max<uint64_t>(waves, ctx->tokens.cap / (kSlabSyms * 4)) * kSlabSyms * 4);
-        if (r) return r;
-        a.wave_bytes = wb;
+        a.wave_bytes = hbm_wb;
         a.scratch = (uint8_t *)ctx->dscratch.p;
-        a.tokens = (uint32_t *)ctx->tokens.p;
-        hipLaunchKernelGGL(deflate_kernel<true>, dim3((unsigned)waves), dim3(64), kCrcTabBytes, st, a);
-        hipError_t e = hipGetLastError();
+        hipLaunchKernelGGL(deflate_kernel<true>, dim3((unsigned)hbm_waves), dim3(64), kCrcTabBytes, st, a);
+        e = hipGetLastError();
         if (e != hipSuccess) {
             set_err("deflate_kernel<hbm>", e);
             return PMC_E_NO_DEVICE;
@@ -521,4 +553,11 @@ PMC_API int pmc_route_keys(uint64_t first, uint32_t n, uint32_t num_shards, uint
     hipLaunchKernelGGL(route_kernel, grid_for(n), dim3(256), 0, (hipStream_t)stream, first, n, num_shards, n_gpus,
                        gpu);
     return hipGetLastError() == hipSuccess ? PMC_OK : PMC_E_NO_DEVICE;
+}
+
+// Diagnostics: device buffer of 8 uint64 that PMC_STAMPS builds add per-phase cycles into.
+PMC_API int pmc_debug_stamps(pmc_ctx *ctx, uint64_t *dev_buf) {
+    if (!ctx) return PMC_E_ARG;
+    ctx->dbg = dev_buf;
+    return PMC_OK;
 }

@@ -137,6 +137,16 @@ struct DeflateWave {
     uint32_t *tok; // per-wave HBM symbol slab (kSymsPerBlock entries)
     const uint32_t *crc_tab;
     uint64_t out_words;
+    // diagnostic phase stamps (PMC_STAMPS builds only; never quoted as timings)
+    uint64_t st[8];
+    uint64_t t_last;
+    __device__ void stamp(int k) {
+#ifdef PMC_STAMPS
+        uint64_t t = __builtin_amdgcn_s_memtime();
+        st[k] += t - t_last;
+        t_last = t;
+#endif
+    }
 
     __device__ void sync() {
         if (kHbm) wave_sync_global();
@@ -268,6 +278,7 @@ struct DeflateWave {
         // trees + sizes on lane 0
         uint32_t opt_lenb = 0, static_lenb = 0;
         int l_max = 0, d_max = 0, mbi = 0;
+        stamp(2);
         if (l == 0) {
             BlockPlan p = plan_block(*tr, T);
             opt_lenb = p.opt_lenb;
@@ -277,6 +288,7 @@ struct DeflateWave {
             mbi = p.max_blindex;
         }
         sync();
+        stamp(3);
         opt_lenb = rfl(opt_lenb);
         static_lenb = rfl(static_lenb);
         l_max = rfl(l_max);
@@ -343,6 +355,7 @@ struct DeflateWave {
         sync();
         if (l == 0) tr->ltree[kEndBlock].fc = 1;
         sync();
+        stamp(4);
         return bitpos;
     }
 
@@ -364,11 +377,13 @@ struct DeflateWave {
         }
         sync();
         const uint32_t crc = wave_crc32(b, (uint32_t)len, crc_tab);
+        stamp(0);
         // 2. hash + sort
         const uint64_t npos = len >= kMinMatch ? len - (kMinMatch - 1) : 0;
         if (npos) sort_positions(npos);
         for (uint64_t k = l; k < out_words; k += 64) outw[k] = 0;
         sync();
+        stamp(1);
         if (l < 10) {
             const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 2, 3};
             outb[l] = hdr[l];
@@ -456,6 +471,7 @@ struct DeflateWave {
             for (uint64_t k = l; k < nbytes; k += 64) dst[k] = outb[k];
         }
         if (l == 0) *dst_len = (uint32_t)nbytes;
+        stamp(5);
         return 0;
     }
 };
@@ -488,6 +504,10 @@ __global__ void __launch_bounds__(256) deflate_kernel(DeflateArgs a) {
     W.out_words = L.out_words;
     W.tok = a.tokens + wave * kSymsPerBlock;
     W.crc_tab = crc_tab;
+    for (int k = 0; k < 8; k++) W.st[k] = 0;
+#ifdef PMC_STAMPS
+    W.t_last = __builtin_amdgcn_s_memtime();
+#endif
     // init_block once; flush_block re-initialises after each block
     const int l = lane_id();
     for (int n = l; n < kLCodes; n += 64) W.tr->ltree[n].fc = 0;
@@ -521,6 +541,10 @@ __global__ void __launch_bounds__(256) deflate_kernel(DeflateArgs a) {
         }
       }
     }
+#ifdef PMC_STAMPS
+    if (l == 0 && a.dbg)
+        for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&a.dbg[k], (unsigned long long)W.st[k]);
+#endif
 }
 
 template __global__ void deflate_kernel<false>(DeflateArgs);

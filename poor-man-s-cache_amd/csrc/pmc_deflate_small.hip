@@ -1,0 +1,886 @@
+// pmc_deflate_small.hip -- gzip level-9 compression of values up to 16382 bytes (always a
+// single DEFLATE block: zlib flushes at 16383 symbols), the hot path of the cache
+// (BASELINE configs 2-4: 256 B .. 4 KiB values).  Same output bytes as pmc_deflate.hip /
+// zlib 1.2.11 (reference: /root/reference/src/compressor/gzip_compressor.cpp:3-50); this
+// variant is organised for gfx950 latency and LDS capacity:
+//
+//  * working set ~9n + 3.5 KiB per wave (u16 sorted positions + u16 ranks; the candidate
+//    hash is recomputed from the value bytes; sort scratch aliases the Huffman/output
+//    region), so 12+ waves share a CU at 1 KiB values.
+//  * longest_match: 64 chain candidates per step, LCP by aligned-dword compares; the
+//    winner is taken with one ballot + readlane when at most one lane beats the current
+//    best (the common case) and a DPP row reduction + 4 readlanes otherwise -- no LDS
+//    shuffles on the serial path.  Symbol histograms are built after the parse, in parallel.
+//  * Huffman (zlib trees.c build_tree): the binary heap lives in five VGPRs, lane-distributed
+//    (entry k in lane k%64 of register k/64), driven by scalar code through v_readlane /
+//    v_writelane, so each pqdownheap level costs a few cycles instead of LDS round trips.
+//    Entries pack (freq<<5 | depth)<<10 | node, so zlib's `smaller` is one compare.
+//    Everything around the heap is wave-parallel: leaf compaction (ballot), code lengths
+//    (pointer jumping over the father links), canonical codes (ballot ranks), scan_tree /
+//    send_tree (each maximal run of equal lengths has a fixed code sequence given its
+//    value and length, so runs are encoded independently).  A length-limit overflow (rare)
+//    re-plans the block with the serial zlib restatement (pmc_trees.hpp) on a per-wave
+//    HBM scratch Trees.
+#include <hip/hip_runtime.h>
+
+#include "pmc_device.hpp"
+#include "pmc_kernels.hpp"
+
+namespace pmc {
+
+constexpr uint32_t kSmallMax = 16382;
+
+struct SmallLayout {
+    uint64_t bytes, S, R, freq, W, total;
+    // inside W (flush phase)
+    uint64_t out, lcode, dcode, blcode, dad, dep, runs;
+    uint64_t out_words;
+    // inside W (sort phase)
+    uint64_t T, H, cnt;
+};
+
+__host__ __device__ inline SmallLayout small_layout(uint64_t n) {
+    auto a = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
+    SmallLayout L;
+    uint64_t o = 0;
+    L.bytes = o;
+    o += a(n + 32);
+    L.S = o;
+    o += a(2 * n + 2);
+    L.R = o;
+    o += a(2 * n + 2);
+    L.freq = o; // lfreq u32[288], dfreq u32[32], blfreq u32[32]
+    o += 352 * 4;
+    L.W = o;
+    // flush view
+    uint64_t f = 0;
+    L.out = f;
+    L.out_words = a(gzip_bound(n) + 16) / 4;
+    f += L.out_words * 4;
+    L.lcode = f;
+    f += 288 * 4;
+    L.dcode = f;
+    f += 32 * 4;
+    L.blcode = f;
+    f += 32 * 4;
+    L.dad = f;
+    f += 576 * 2;
+    L.dep = f;
+    f += 576;
+    L.runs = f; // run lengths at run starts: lit/len [0,288), dist [288,320)
+    f += 320 * 2;
+    // sort view
+    uint64_t s = 0;
+    L.T = s;
+    s += a(2 * n + 2);
+    L.H = s;
+    s += a(2 * n + 2);
+    L.cnt = s;
+    s += 16 * 64 * 2;
+    o += a(f > s ? f : s);
+    L.total = a(o);
+    return L;
+}
+uint64_t deflate_small_wave_bytes(uint64_t n) { return small_layout(n).total; }
+
+__device__ __forceinline__ uint32_t hash3(uint32_t w) {
+    return ((w & 0xff) << 10 ^ ((w >> 8) & 0xff) << 5 ^ ((w >> 16) & 0xff)) & 0x7fffu;
+}
+
+// ---- register-resident binary heap ---------------------------------------------------
+struct RegHeap {
+    uint32_t h0, h1, h2, h3, h4; // entry k: lane k&63 of h[k>>6]
+    __device__ uint32_t reg(int r) const {
+        return r == 0 ? h0 : r == 1 ? h1 : r == 2 ? h2 : r == 3 ? h3 : h4;
+    }
+    __device__ uint32_t get(int k) const { return readlane(reg(k >> 6), k & 63); }
+    __device__ void set(int k, uint32_t v) {
+        const int r = k >> 6, ln = k & 63;
+        if (r == 0) h0 = writelane(h0, v, ln);
+        else if (r == 1) h1 = writelane(h1, v, ln);
+        else if (r == 2) h2 = writelane(h2, v, ln);
+        else if (r == 3) h3 = writelane(h3, v, ln);
+        else h4 = writelane(h4, v, ln);
+    }
+    // pqdownheap (trees.c) with smaller(n,m) == key(n) <= key(m), key = e >> 10
+    __device__ void down(int k, int heap_len) {
+        uint32_t v = get(k);
+        int j = k << 1;
+        while (j <= heap_len) {
+            uint32_t x = get(j);
+            if (j < heap_len) {
+                uint32_t y = get(j + 1);
+                if ((y >> 10) <= (x >> 10)) {
+                    j++;
+                    x = y;
+                }
+            }
+            if ((v >> 10) <= (x >> 10)) break;
+            set(k, x);
+            k = j;
+            j <<= 1;
+        }
+        set(k, v);
+    }
+};
+
+struct TreeOut {
+    int max_code;
+    int64_t opt, stat;
+    bool overflow;
+    int dummy[2]; // symbols whose freq build_tree set to 1 (zlib's "at least 2 codes"), or -1
+};
+
+struct SmallWave {
+    uint8_t *b;
+    uint32_t *bw;
+    uint16_t *S, *R;
+    uint32_t *lfreq, *dfreq, *blfreq;
+    uint8_t *W;
+    uint32_t *outw;
+    uint8_t *outb;
+    uint64_t out_words;
+    uint32_t *lcode, *dcode, *blcode;
+    uint16_t *dad;
+    uint8_t *dep;
+    uint16_t *runs;
+    uint16_t *T, *H, *cnt;
+    uint32_t *tok;
+    Trees *fb; // HBM scratch for the serial fallback
+    const uint32_t *crc_tab;
+    uint64_t st[8];
+    uint64_t t_last;
+
+    __device__ void stamp(int k) {
+#ifdef PMC_STAMPS
+        uint64_t t = __builtin_amdgcn_s_memtime();
+        st[k] += t - t_last;
+        t_last = t;
+#endif
+    }
+
+    __device__ uint32_t load4(uint32_t p) const {
+        uint32_t w0 = bw[p >> 2], w1 = bw[(p >> 2) + 1];
+        return __builtin_amdgcn_alignbyte(w1, w0, p & 3);
+    }
+
+    // ---- stable LSD radix sort of positions by hash: 4 x 4-bit passes -------------------
+    __device__ __noinline__ void sort_positions(uint32_t npos) {
+        const int l = lane_id();
+        for (uint32_t p = l; p < npos; p += 64) H[p] = (uint16_t)hash3(load4(p));
+        const uint32_t c = (npos + 63) / 64;
+        const uint32_t beg = (uint32_t)l * c;
+        wave_sync();
+        for (int pass = 0; pass < 4; pass++) {
+            const int sh = 4 * pass;
+            const uint16_t *src = pass == 0 ? nullptr : (pass & 1 ? T : S);
+            uint16_t *dst = pass & 1 ? S : T;
+            for (int d = 0; d < 16; d++) cnt[d * 64 + l] = 0;
+            wave_sync();
+            for (uint32_t j = 0; j < c; j++) {
+                uint32_t idx = beg + j;
+                if (idx < npos) {
+                    uint32_t p = src ? src[idx] : idx;
+                    cnt[((H[p] >> sh) & 15) * 64 + l]++;
+                }
+            }
+            wave_sync();
+            // exclusive scan of the 1024 counters in (digit, lane) order; lane l owns 16
+            uint32_t v[16], s = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                v[k] = cnt[l * 16 + k];
+                s += v[k];
+            }
+            uint32_t base = wave_incl_scan(s) - s;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                cnt[l * 16 + k] = (uint16_t)base;
+                base += v[k];
+            }
+            wave_sync();
+            for (uint32_t j = 0; j < c; j++) {
+                uint32_t idx = beg + j;
+                if (idx < npos) {
+                    uint32_t p = src ? src[idx] : idx;
+                    uint32_t slot = ((H[p] >> sh) & 15) * 64 + l;
+                    uint32_t at = cnt[slot];
+                    cnt[slot] = (uint16_t)(at + 1);
+                    dst[at] = (uint16_t)p;
+                }
+            }
+            wave_sync();
+        }
+        for (uint32_t k = l; k < npos; k += 64) R[S[k]] = (uint16_t)k;
+        wave_sync();
+    }
+
+    // ---- longest_match over the sorted chain -------------------------------------------
+    // Returns the match length (> b0) or 0; *q_out = nearest candidate achieving it.
+    __device__ uint32_t search(uint32_t i, uint32_t b0, uint32_t len, uint32_t *q_out) {
+        const int l = lane_id();
+        const uint32_t C = b0 >= 32 ? 1024u : 4096u;
+        const uint32_t nice = (len - i) < 258 ? (len - i) : 258;
+        const uint32_t wi = load4(i);
+        const uint32_t hi = hash3(wi);
+        const int r = (int)R[i];
+        uint32_t examined = 0, best = 0, bestq = 0;
+        for (int kb = r - 1;; kb -= 64) {
+            const int k = kb - l;
+            const uint32_t ord = examined + (uint32_t)l;
+            uint32_t q = k >= 0 ? S[k] : 0u;
+            uint32_t wq = load4(q);
+            // position 0 is zlib's NIL (head[] value 0): never a match source; it is the
+            // lowest position of its hash run, so valid lanes stay a prefix
+            bool valid = k >= 0 && q != 0 && hash3(wq) == hi && ord < C;
+            uint64_t m = ballot(valid);
+            uint32_t npre = ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m);
+            if (npre == 0) break;
+            uint32_t cl = 0;
+            if ((uint32_t)l < npre) {
+                uint32_t x = wi ^ wq;
+                if (x) {
+                    cl = (uint32_t)__builtin_ctz(x) >> 3;
+                } else {
+                    cl = 4;
+                    while (cl < nice) {
+                        x = load4(i + cl) ^ load4(q + cl);
+                        if (x) {
+                            cl += (uint32_t)__builtin_ctz(x) >> 3;
+                            break;
+                        }
+                        cl += 4;
+                    }
+                }
+                cl = cl < nice ? cl : nice;
+            }
+            const uint32_t thr = best > b0 ? best : b0;
+            uint64_t mm = ballot(cl > thr);
+            if (mm) {
+                int src;
+                if ((mm & (mm - 1)) == 0) {
+                    src = __builtin_ctzll(mm);
+                } else {
+                    uint32_t key = cl > thr ? (cl << 16) | (0xffffu - ord) : 0u;
+                    uint32_t mx = wave_max_dpp(key);
+                    src = (int)(0xffffu - (mx & 0xffffu) - examined);
+                }
+                best = readlane(cl, src);
+                bestq = readlane(q, src);
+            }
+            examined += npre;
+            if (best >= nice || npre < 64 || examined >= C) break;
+        }
+        *q_out = bestq;
+        return best > b0 ? best : 0u;
+    }
+
+    // ---- Huffman: build_tree for one tree -------------------------------------------------
+    // freq[0..elems) in LDS (u32).  Writes code_out[s] = bitrev code | len << 16 for
+    // s <= max_code (0 for unused), returns zlib's opt_len/static_len contributions.
+    __device__ __noinline__ TreeOut build_tree(uint32_t *freq, int elems, const CtData *stree, const uint8_t *extra,
+                                  int extra_base, int max_length, uint32_t *code_out) {
+        const int l = lane_id();
+        TreeOut to{};
+        // 1. leaves in symbol order -> staging (code_out reused) at heap index 1..k
+        int heap_len = 0, max_code = -1;
+        for (int c0 = 0; c0 < elems; c0 += 64) {
+            const int s = c0 + l;
+            const uint32_t f = s < elems ? freq[s] : 0u;
+            const uint64_t nz = ballot(f != 0);
+            if (f) code_out[heap_len + 1 + popc_lt(nz)] = ((f << 5) << 10) | (uint32_t)s;
+            if (nz) max_code = c0 + 63 - __builtin_clzll(nz);
+            heap_len += __builtin_popcountll(nz);
+        }
+        wave_sync();
+        // dummies (build_tree: while (heap_len < 2))
+        int64_t opt = 0, stat = 0;
+        to.dummy[0] = to.dummy[1] = -1;
+        while (heap_len < 2) {
+            const int node = max_code < 2 ? ++max_code : 0;
+            to.dummy[to.dummy[0] < 0 ? 0 : 1] = node;
+            if (l == 0) {
+                code_out[++heap_len] = ((1u << 5) << 10) | (uint32_t)node;
+                freq[node] = 1;
+            } else {
+                ++heap_len;
+            }
+            opt -= 1;
+            if (stree) stat -= stree[node].dl;
+        }
+        wave_sync();
+        RegHeap hp;
+        hp.h0 = code_out[l];
+        hp.h1 = code_out[64 + l];
+        hp.h2 = code_out[128 + l];
+        hp.h3 = code_out[192 + l];
+        hp.h4 = code_out[256 + l < 288 ? 256 + l : 287];
+        // 2. heapify + merge (all uniform scalar control; the heap never leaves VGPRs)
+        for (int n = heap_len / 2; n >= 1; n--) hp.down(n, heap_len);
+        int node = elems;
+        bool deep = false;
+        do {
+            const uint32_t n = hp.get(1);
+            hp.set(1, hp.get(heap_len));
+            heap_len--;
+            hp.down(1, heap_len);
+            const uint32_t m = hp.get(1);
+            const uint32_t kn = n >> 10, km = m >> 10;
+            const uint32_t dn = kn & 31, dm = km & 31;
+            const uint32_t d = (dn >= dm ? dn : dm) + 1;
+            deep |= d >= 31;
+            const uint32_t key = (((kn >> 5) + (km >> 5)) << 5) | (d & 31);
+            if (l == 0) {
+                dad[n & 1023] = (uint16_t)node;
+                dad[m & 1023] = (uint16_t)node;
+            }
+            hp.set(1, (key << 10) | (uint32_t)node);
+            node++;
+            hp.down(1, heap_len);
+        } while (heap_len >= 2);
+        const int root = node - 1;
+        if (l == 0) dad[root] = (uint16_t)root;
+        wave_sync();
+        // 3. depth of every node by pointer jumping over the father links (depth <= 21)
+        for (int x = l; x < node; x += 64) {
+            bool in_tree = x >= elems || (x <= max_code && freq[x] != 0);
+            if (!in_tree) dad[x] = (uint16_t)x;
+            dep[x] = (in_tree && x != root) ? 1 : 0;
+        }
+        wave_sync();
+        for (int it = 0; it < 5; it++) {
+            uint32_t na[9], nd[9];
+#pragma unroll
+            for (int j = 0; j < 9; j++) {
+                int x = l + 64 * j;
+                if (x < node) {
+                    uint32_t a = dad[x];
+                    na[j] = dad[a];
+                    nd[j] = (uint32_t)dep[x] + dep[a];
+                }
+            }
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < 9; j++) {
+                int x = l + 64 * j;
+                if (x < node) {
+                    dad[x] = (uint16_t)na[j];
+                    dep[x] = (uint8_t)nd[j];
+                }
+            }
+            wave_sync();
+        }
+        // 4. code lengths, overflow check, opt_len / static_len sums
+        uint32_t over = 0;
+        int64_t po = 0, ps = 0;
+        for (int s = l; s <= max_code; s += 64) {
+            uint32_t f = freq[s];
+            uint32_t len = f ? dep[s] : 0u;
+            over |= len > (uint32_t)max_length;
+            uint32_t xb = s >= extra_base ? extra[s - extra_base] : 0u;
+            po += (int64_t)f * (len + xb);
+            if (stree) ps += (int64_t)f * (stree[s].dl + xb);
+        }
+        over = ballot(over != 0) != 0 || deep;
+        to.overflow = over;
+        po = (int64_t)wave_sum_u32((uint32_t)po);
+        ps = (int64_t)wave_sum_u32((uint32_t)ps);
+        to.opt = opt + po;
+        to.stat = stat + ps;
+        to.max_code = max_code;
+        if (over) return to;
+        // 5. gen_codes: canonical code = next_code[len] + rank among equal lengths
+        uint32_t bl_count[16];
+#pragma unroll
+        for (int L = 0; L < 16; L++) bl_count[L] = 0;
+        for (int c0 = 0; c0 <= max_code; c0 += 64) {
+            const int s = c0 + l;
+            const uint32_t len = (s <= max_code && freq[s]) ? dep[s] : 0u;
+#pragma unroll
+            for (int L = 1; L <= 15; L++) bl_count[L] += __builtin_popcountll(ballot(len == (uint32_t)L));
+        }
+        uint32_t next_code[16];
+        uint32_t code = 0;
+        next_code[0] = 0;
+#pragma unroll
+        for (int L = 1; L <= 15; L++) {
+            code = (code + (L > 1 ? bl_count[L - 1] : 0u)) << 1;
+            next_code[L] = code;
+        }
+        // (every entry below elems is written: the staging area left heap entries there)
+        for (int c0 = 0; c0 < elems; c0 += 64) {
+            const int s = c0 + l;
+            const uint32_t len = (s <= max_code && freq[s]) ? dep[s] : 0u;
+            uint32_t mycode = 0;
+#pragma unroll
+            for (int L = 1; L <= 15; L++) {
+                const uint64_t mk = ballot(len == (uint32_t)L);
+                if (len == (uint32_t)L) mycode = next_code[L] + popc_lt(mk);
+                next_code[L] += __builtin_popcountll(mk);
+            }
+            if (s < elems)
+                code_out[s] = len ? ((__builtin_bitreverse32(mycode) >> (32 - len)) | (len << 16)) : 0u;
+        }
+        wave_sync();
+        return to;
+    }
+
+    // per maximal run of code lengths (value v, length R): bl-code counts (scan_tree)
+    __device__ static void run_counts(uint32_t v, uint32_t R, uint32_t *blfreq) {
+        if (v) {
+            uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = rem / 6, last = rem % 6;
+            uint32_t nv = (c1 < 4 ? c1 : 1) + (last < 3 ? last : 0);
+            uint32_t n16 = (c1 >= 4 ? 1 : 0) + full + (last >= 3 ? 1 : 0);
+            if (nv) atomicAdd(&blfreq[v], nv);
+            if (n16) atomicAdd(&blfreq[16], n16);
+        } else {
+            uint32_t full = R / 138, last = R % 138;
+            uint32_t n18 = full + (last > 10 ? 1 : 0), n17 = (last >= 3 && last <= 10) ? 1 : 0;
+            uint32_t n0 = last < 3 ? last : 0;
+            if (n0) atomicAdd(&blfreq[0], n0);
+            if (n17) atomicAdd(&blfreq[17], n17);
+            if (n18) atomicAdd(&blfreq[18], n18);
+        }
+    }
+    // bits of one run (send_tree); emit into the image at pos when out != nullptr
+    __device__ uint32_t run_bits(uint32_t v, uint32_t R, uint64_t pos, bool write) {
+        auto put = [&](uint32_t c, uint32_t xv, uint32_t xn, uint32_t &acc) {
+            uint32_t cw = blcode[c], cn = cw >> 16;
+            if (write) {
+                uint64_t bits = (uint64_t)(cw & 0xffff) | ((uint64_t)xv << cn);
+                or_bits_lds(pos + acc, bits, (int)(cn + xn));
+            }
+            acc += cn + xn;
+        };
+        uint32_t acc = 0;
+        if (v) {
+            uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = rem / 6, last = rem % 6;
+            if (c1 < 4) {
+                for (uint32_t k = 0; k < c1; k++) put(v, 0, 0, acc);
+            } else {
+                put(v, 0, 0, acc);
+                put(16, c1 - 4, 2, acc);
+            }
+            for (uint32_t k = 0; k < full; k++) put(16, 3, 2, acc);
+            if (last) {
+                if (last < 3) {
+                    for (uint32_t k = 0; k < last; k++) put(v, 0, 0, acc);
+                } else {
+                    put(16, last - 3, 2, acc);
+                }
+            }
+        } else {
+            uint32_t full = R / 138, last = R % 138;
+            for (uint32_t k = 0; k < full; k++) put(18, 127, 7, acc);
+            if (last) {
+                if (last < 3) {
+                    for (uint32_t k = 0; k < last; k++) put(0, 0, 0, acc);
+                } else if (last <= 10) {
+                    put(17, last - 3, 3, acc);
+                } else {
+                    put(18, last - 11, 7, acc);
+                }
+            }
+        }
+        return acc;
+    }
+    __device__ void or_bits_lds(uint64_t pos, uint64_t v, int n) {
+        if (n == 0) return;
+        uint64_t w = pos >> 5;
+        int s = (int)(pos & 31);
+        uint32_t lo = (uint32_t)(v << s);
+        uint32_t mid = (uint32_t)(s ? (v >> (32 - s)) : (v >> 32));
+        uint32_t hi = s ? (uint32_t)(v >> (64 - s)) : 0u;
+        if (lo) atomicOr(&outw[w], lo);
+        if (n + s > 32 && mid) atomicOr(&outw[w + 1], mid);
+        if (n + s > 64 && hi) atomicOr(&outw[w + 2], hi);
+    }
+
+    // scan_tree for lengths code[0..max_code]: records run lengths at run starts into
+    // runR (u16) and adds the bl counts.  Chunks are walked back to front so each run
+    // start knows where the next run begins.
+    __device__ void scan_runs(const uint32_t *code, int max_code, uint16_t *runR) {
+        const int l = lane_id();
+        int next_start = max_code + 1;
+        for (int c0 = (max_code / 64) * 64; c0 >= 0; c0 -= 64) {
+            const int s = c0 + l;
+            const bool in = s <= max_code;
+            const uint32_t v = in ? code[s] >> 16 : 0xffffu;
+            const uint32_t vp = (in && s > 0) ? code[s - 1] >> 16 : 0xfffeu;
+            const bool start = in && (s == 0 || v != vp);
+            const uint64_t m = ballot(start);
+            const uint64_t above = l == 63 ? 0 : (m & (~0ull << (l + 1)));
+            const int nxt = above ? c0 + __builtin_ctzll(above) : next_start;
+            if (start) {
+                runR[s] = (uint16_t)(nxt - s);
+                run_counts(v, (uint32_t)(nxt - s), blfreq);
+            }
+            if (m) next_start = c0 + __builtin_ctzll(m);
+        }
+    }
+    // send_tree: every run start writes its symbols at its prefix offset; returns bits
+    __device__ uint64_t send_runs(const uint32_t *code, int max_code, const uint16_t *runR, uint64_t pos) {
+        const int l = lane_id();
+        uint64_t base = pos;
+        for (int c0 = 0; c0 <= max_code; c0 += 64) {
+            const int s = c0 + l;
+            const bool in = s <= max_code;
+            const uint32_t v = in ? code[s] >> 16 : 0u;
+            const uint32_t vp = (in && s > 0) ? code[s - 1] >> 16 : 0xfffeu;
+            const bool start = in && (s == 0 || v != vp);
+            const uint32_t R = start ? runR[s] : 0u;
+            const uint32_t nb = start ? run_bits(v, R, 0, false) : 0u;
+            const uint32_t incl = wave_incl_scan(nb);
+            if (start) run_bits(v, R, base + incl - nb, true);
+            base += readlane(incl, 63);
+        }
+        return base - pos;
+    }
+
+    // ---- block flush: trees, block type, emission (single final block) --------------------
+    __device__ __noinline__ uint64_t flush(uint32_t ntok, uint32_t len, uint64_t bitpos) {
+        const int l = lane_id();
+        const Tables &TT = c_tables;
+        // histograms from the symbol slab
+        for (int s = l; s < 352; s += 64) lfreq[s] = 0; // lfreq, dfreq, blfreq contiguous
+        wave_sync();
+        for (uint32_t t = l; t < ntok; t += 64) {
+            const uint32_t tk = tok[t], dist = tk >> 16, lc = tk & 0xff;
+            if (dist == 0) {
+                atomicAdd(&lfreq[lc], 1u);
+            } else {
+                atomicAdd(&lfreq[TT.length_code[lc] + kLiterals + 1], 1u);
+                atomicAdd(&dfreq[d_code(TT, dist - 1)], 1u);
+            }
+        }
+        if (l == 0) lfreq[kEndBlock] = 1;
+        wave_sync();
+        stamp(2);
+        TreeOut tl = build_tree(lfreq, kLCodes, TT.static_ltree, TT.extra_lbits, kLiterals + 1, kMaxBits, lcode);
+        TreeOut td = build_tree(dfreq, kDCodes, TT.static_dtree, TT.extra_dbits, 0, kMaxBits, dcode);
+        // (not in dad[]: the bit-length tree's build_tree below reuses dad[])
+        uint16_t *runL = runs, *runD = runs + 288;
+        TreeOut tb{};
+        int mbi = 0;
+        bool fallback = tl.overflow || td.overflow;
+        if (!fallback) {
+            scan_runs(lcode, tl.max_code, runL);
+            scan_runs(dcode, td.max_code, runD);
+            wave_sync();
+            tb = build_tree(blfreq, kBLCodes, nullptr, TT.extra_blbits, 0, kMaxBLBits, blcode);
+            fallback = tb.overflow;
+        }
+        int64_t opt_len = 0, static_len = 0;
+        int l_max = tl.max_code, d_max = td.max_code;
+        if (!fallback) {
+            for (mbi = kBLCodes - 1; mbi >= 3; mbi--)
+                if ((blcode[TT.bl_order[mbi]] >> 16) != 0) break;
+            opt_len = tl.opt + td.opt + tb.opt + 3 * ((int64_t)mbi + 1) + 5 + 5 + 4;
+            static_len = tl.stat + td.stat;
+        } else {
+            // serial zlib restatement on HBM scratch (length-limit overflow: rare).  It starts
+            // from the real frequencies: undo the dummy leaves build_tree added above.
+            for (int s = l; s < kLCodes; s += 64) {
+                const bool dm = s == tl.dummy[0] || s == tl.dummy[1];
+                fb->ltree[s] = CtData{(uint16_t)(dm ? 0u : lfreq[s]), 0};
+            }
+            if (l < kDCodes) {
+                const bool dm = l == td.dummy[0] || l == td.dummy[1];
+                fb->dtree[l] = CtData{(uint16_t)(dm ? 0u : dfreq[l]), 0};
+            }
+            if (l < kBLCodes) fb->bltree[l] = CtData{0, 0};
+            wave_sync_global();
+            uint32_t ol = 0, sl = 0;
+            if (l == 0) {
+                BlockPlan p = plan_block(*fb, TT);
+                ol = p.opt_lenb;
+                sl = p.static_lenb;
+                l_max = p.l_max;
+                d_max = p.d_max;
+                mbi = p.max_blindex;
+            }
+            wave_sync_global();
+            ol = rfl(ol);
+            sl = rfl(sl);
+            l_max = rfl(l_max);
+            d_max = rfl(d_max);
+            mbi = rfl(mbi);
+            for (int s = l; s < 288; s += 64)
+                lcode[s] = s <= l_max ? (uint32_t)fb->ltree[s].fc | ((uint32_t)fb->ltree[s].dl << 16) : 0u;
+            if (l < 32) dcode[l] = l <= d_max ? (uint32_t)fb->dtree[l].fc | ((uint32_t)fb->dtree[l].dl << 16) : 0u;
+            wave_sync();
+            // express the plan's byte sizes as bit totals with the same rounding
+            opt_len = (int64_t)ol * 8 - 10;
+            static_len = (int64_t)sl * 8 - 10;
+        }
+        stamp(3);
+        const uint32_t opt_lenb_raw = (uint32_t)(((uint64_t)opt_len + 3 + 7) >> 3);
+        const uint32_t static_lenb = (uint32_t)(((uint64_t)static_len + 3 + 7) >> 3);
+        const uint32_t opt_lenb = static_lenb <= opt_lenb_raw ? static_lenb : opt_lenb_raw;
+        const uint32_t stored_len = len;
+        if (stored_len + 4 <= opt_lenb) {
+            // stored block (last): header, align, LEN, NLEN, bytes
+            if (l == 0) or_bits_lds(bitpos, 1u, 3);
+            bitpos = (bitpos + 3 + 7) & ~(uint64_t)7;
+            const uint64_t o = bitpos >> 3;
+            wave_sync();
+            if (l < 4) {
+                uint32_t v = l < 2 ? stored_len : ~stored_len;
+                outb[o + l] = (uint8_t)(v >> (8 * (l & 1)));
+            }
+            for (uint32_t k = l; k < stored_len; k += 64) outb[o + 4 + k] = b[k];
+            bitpos += (4 + (uint64_t)stored_len) * 8;
+            wave_sync();
+            return bitpos;
+        }
+        const bool fixed = static_lenb == opt_lenb;
+        if (fixed) {
+            for (int s = l; s < 288; s += 64)
+                lcode[s] = s < kLCodes ? (uint32_t)TT.static_ltree[s].fc | ((uint32_t)TT.static_ltree[s].dl << 16) : 0u;
+            if (l < 32) dcode[l] = l < kDCodes ? (uint32_t)TT.static_dtree[l].fc | ((uint32_t)TT.static_dtree[l].dl << 16) : 0u;
+            if (l == 0) or_bits_lds(bitpos, (1u << 1) | 1u, 3);
+            bitpos += 3;
+            wave_sync();
+        } else {
+            const int lcodes = l_max + 1, dcodes = d_max + 1, blcodes = mbi + 1;
+            if (fallback) {
+                uint64_t hb = 0;
+                if (l == 0) {
+                    LaneBitsL lb{outw, bitpos};
+                    lb.put((2u << 1) | 1u, 3);
+                    BlockPlan p{0, 0, l_max, d_max, mbi};
+                    send_all_trees(*fb, TT, lb, p);
+                    hb = lb.pos;
+                }
+                bitpos = rfl64(hb);
+                wave_sync();
+            } else {
+                if (l == 0) {
+                    or_bits_lds(bitpos, (2u << 1) | 1u, 3);
+                    or_bits_lds(bitpos + 3, (uint32_t)(lcodes - 257), 5);
+                    or_bits_lds(bitpos + 8, (uint32_t)(dcodes - 1), 5);
+                    or_bits_lds(bitpos + 13, (uint32_t)(blcodes - 4), 4);
+                }
+                if (l < blcodes) or_bits_lds(bitpos + 17 + 3 * l, blcode[TT.bl_order[l]] >> 16, 3);
+                bitpos += 17 + 3 * (uint64_t)blcodes;
+                wave_sync();
+                bitpos += send_runs(lcode, lcodes - 1, runL, bitpos);
+                bitpos += send_runs(dcode, dcodes - 1, runD, bitpos);
+                wave_sync();
+            }
+        }
+        // symbols
+        for (uint32_t t0 = 0; t0 < ntok; t0 += 64) {
+            const uint32_t t = t0 + (uint32_t)l;
+            uint32_t nb = 0;
+            uint64_t v = 0;
+            if (t < ntok) {
+                const uint32_t tk = tok[t], dist = tk >> 16, lc = tk & 0xff;
+                if (dist == 0) {
+                    const uint32_t c = lcode[lc];
+                    v = c & 0xffff;
+                    nb = c >> 16;
+                } else {
+                    const uint32_t code = TT.length_code[lc];
+                    uint32_t c = lcode[code + kLiterals + 1];
+                    v = c & 0xffff;
+                    nb = c >> 16;
+                    const uint32_t xl = TT.extra_lbits[code];
+                    v |= (uint64_t)((lc - TT.base_length[code]) & ((1u << xl) - 1)) << nb;
+                    nb += xl;
+                    const uint32_t dm = dist - 1, dc = d_code(TT, dm);
+                    c = dcode[dc];
+                    v |= (uint64_t)(c & 0xffff) << nb;
+                    nb += c >> 16;
+                    const uint32_t xd = TT.extra_dbits[dc];
+                    v |= (uint64_t)((dm - TT.base_dist[dc]) & ((1u << xd) - 1)) << nb;
+                    nb += xd;
+                }
+            }
+            const uint32_t incl = wave_incl_scan(nb);
+            if (nb) or_bits_lds(bitpos + incl - nb, v, (int)nb);
+            bitpos += readlane(incl, 63);
+        }
+        const uint32_t eob = lcode[kEndBlock];
+        wave_sync();
+        if (l == 0) or_bits_lds(bitpos, eob & 0xffff, (int)(eob >> 16));
+        bitpos += eob >> 16;
+        bitpos = (bitpos + 7) & ~(uint64_t)7;
+        wave_sync();
+        return bitpos;
+    }
+
+    // bit sink for the serial fallback's send_all_trees (lane 0)
+    struct LaneBitsL {
+        uint32_t *out;
+        uint64_t pos;
+        __device__ void put(unsigned v, int n) {
+            if (n == 0) return;
+            uint64_t w = pos >> 5;
+            int s = (int)(pos & 31);
+            uint64_t x = (uint64_t)(v & ((n >= 32) ? 0xffffffffu : ((1u << n) - 1))) << s;
+            out[w] |= (uint32_t)x;
+            if ((uint32_t)(x >> 32)) out[w + 1] |= (uint32_t)(x >> 32);
+            pos += (uint64_t)n;
+        }
+    };
+
+    // ---- one value ----------------------------------------------------------------------
+    __device__ int run(const uint8_t *src, uint32_t len, uint8_t *dst, uint32_t dst_cap, uint32_t *dst_len) {
+        const int l = lane_id();
+        const uint32_t padded = (len + 32) & ~3u;
+        if ((((uintptr_t)src) & 3) == 0) {
+            const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src);
+            const uint32_t full = len >> 2;
+            for (uint32_t k = l; k < padded / 4; k += 64) bw[k] = k < full ? s4[k] : 0u;
+            wave_sync();
+            if ((uint32_t)l < (len & 3)) b[full * 4 + l] = src[full * 4 + l];
+        } else {
+            for (uint32_t k = l; k < padded / 4; k += 64) bw[k] = 0;
+            wave_sync();
+            for (uint32_t k = l; k < len; k += 64) b[k] = src[k];
+        }
+        wave_sync();
+        const uint32_t crc = wave_crc32(b, len, crc_tab);
+        stamp(0);
+        const uint32_t npos = len >= 3 ? len - 2 : 0;
+        if (npos) sort_positions(npos);
+        stamp(1);
+        // deflate_slow over the sorted chains (single block: len < 16383 symbols)
+        uint32_t i = 0, match_length = 2, prev_length, ntok = 0, treg = 0;
+        uint32_t match_start = 0, prev_match;
+        bool match_available = false;
+        auto emit = [&](uint32_t token) {
+            if ((uint32_t)l == (ntok & 63)) treg = token;
+            if ((ntok & 63) == 63) tok[ntok - 63 + l] = treg;
+            ntok++;
+        };
+        while (i < len) {
+            prev_length = match_length;
+            prev_match = match_start;
+            match_length = 2;
+            if (i + 3 <= len && prev_length < 258) {
+                uint32_t q = 0;
+                const uint32_t m = search(i, prev_length, len, &q);
+                if (m) {
+                    match_length = m;
+                    match_start = q;
+                    if (m == 3 && i - q > 4096) match_length = 2;
+                }
+            }
+            if (prev_length >= 3 && match_length <= prev_length) {
+                emit(((i - 1 - prev_match) << 16) | (prev_length - 3));
+                i += prev_length - 1;
+                match_available = false;
+                match_length = 2;
+            } else if (match_available) {
+                emit(b[i - 1]);
+                i++;
+            } else {
+                match_available = true;
+                i++;
+            }
+        }
+        if (match_available) emit(b[i - 1]);
+        if ((ntok & 63) != 0 && (uint32_t)l < (ntok & 63)) tok[(ntok & ~63u) + l] = treg;
+        wave_sync_global();
+        // flush: the output image aliases the (dead) sort scratch
+        for (uint64_t k = l; k < out_words; k += 64) outw[k] = 0;
+        wave_sync();
+        if (l < 10) {
+            const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 2, 3};
+            outb[l] = hdr[l];
+        }
+        wave_sync();
+        uint64_t bitpos = flush(ntok, len, 80);
+        stamp(4);
+        uint64_t nbytes = bitpos >> 3;
+        if (l < 8) {
+            uint32_t v = l < 4 ? crc : len;
+            outb[nbytes + l] = (uint8_t)(v >> (8 * (l & 3)));
+        }
+        nbytes += 8;
+        wave_sync();
+        if (nbytes > dst_cap) return PMC_E_CAPACITY_DEV;
+        if ((((uintptr_t)dst) & 3) == 0) {
+            uint32_t *d4 = reinterpret_cast<uint32_t *>(dst);
+            const uint64_t full = nbytes >> 2;
+            for (uint64_t k = l; k < full; k += 64) d4[k] = outw[k];
+            if ((uint64_t)l < (nbytes & 3)) dst[full * 4 + l] = outb[full * 4 + l];
+        } else {
+            for (uint64_t k = l; k < nbytes; k += 64) dst[k] = outb[k];
+        }
+        if (l == 0) *dst_len = (uint32_t)nbytes;
+        stamp(5);
+        return 0;
+    }
+};
+
+__global__ void __launch_bounds__(256) deflate_small_kernel(DeflateArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
+    __syncthreads();
+    const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + wib;
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    uint8_t *base = lds + 1024 + (uint64_t)wib * a.wave_bytes;
+    const SmallLayout L = small_layout(a.cap_len);
+    SmallWave w;
+    w.b = base + L.bytes;
+    w.bw = reinterpret_cast<uint32_t *>(base + L.bytes);
+    w.S = reinterpret_cast<uint16_t *>(base + L.S);
+    w.R = reinterpret_cast<uint16_t *>(base + L.R);
+    w.lfreq = reinterpret_cast<uint32_t *>(base + L.freq);
+    w.dfreq = w.lfreq + 288;
+    w.blfreq = w.dfreq + 32;
+    w.W = base + L.W;
+    w.outw = reinterpret_cast<uint32_t *>(w.W + L.out);
+    w.outb = w.W + L.out;
+    w.out_words = L.out_words;
+    w.lcode = reinterpret_cast<uint32_t *>(w.W + L.lcode);
+    w.dcode = reinterpret_cast<uint32_t *>(w.W + L.dcode);
+    w.blcode = reinterpret_cast<uint32_t *>(w.W + L.blcode);
+    w.dad = reinterpret_cast<uint16_t *>(w.W + L.dad);
+    w.dep = w.W + L.dep;
+    w.runs = reinterpret_cast<uint16_t *>(w.W + L.runs);
+    w.T = reinterpret_cast<uint16_t *>(w.W + L.T);
+    w.H = reinterpret_cast<uint16_t *>(w.W + L.H);
+    w.cnt = reinterpret_cast<uint16_t *>(w.W + L.cnt);
+    w.tok = a.tokens + wave * kSlabSyms;
+    w.fb = reinterpret_cast<Trees *>(a.scratch + wave * sizeof(Trees));
+    w.crc_tab = crc_tab;
+    for (int k = 0; k < 8; k++) w.st[k] = 0;
+#ifdef PMC_STAMPS
+    w.t_last = __builtin_amdgcn_s_memtime();
+#endif
+    for (uint64_t g = wave * 64; g < a.n; g += nwaves * 64) {
+        const uint64_t vl = g + (uint64_t)l;
+        const uint32_t myl = vl < a.n ? a.src_len[vl] : 0u;
+        uint64_t todo = ballot(vl < a.n && myl <= a.lds_max_len);
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint64_t v = g + (uint64_t)j;
+            const uint32_t len = readlane(myl, j);
+            if (len == 0) {
+                if (l == 0) {
+                    a.rc[v] = PMC_INVALID_INPUT_DEV;
+                    a.dst_len[v] = 0;
+                }
+                continue;
+            }
+            int rc = w.run(a.src + a.src_off[v], len, a.dst + a.dst_off[v], a.dst_cap[v], a.dst_len + v);
+            if (l == 0) {
+                a.rc[v] = rc;
+                if (rc) a.dst_len[v] = 0;
+            }
+        }
+    }
+#ifdef PMC_STAMPS
+    if (l == 0 && a.dbg)
+        for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&a.dbg[k], (unsigned long long)w.st[k]);
+#endif
+}
+
+} // namespace pmc

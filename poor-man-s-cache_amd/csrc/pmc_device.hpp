@@ -82,6 +82,42 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v) {
     return v;
 }
 
+// ---- DPP-based wave primitives (no LDS round trip) --------------------------------------
+// row-level butterfly with quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror:
+// afterwards every lane holds the max of its 16-lane row.
+__device__ __forceinline__ uint32_t dpp_row_max(uint32_t v) {
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);
+    v = t > v ? t : v;
+    return v;
+}
+// max over the wave, result uniform (SGPR).  All 64 lanes must be active.
+__device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
+    v = dpp_row_max(v);
+    uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    a = a > b ? a : b;
+    c = c > d ? c : d;
+    return a > c ? a : c;
+}
+__device__ __forceinline__ uint32_t readlane(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+// v_writelane without inline asm: compare + select (2 VALU, no hazards to pad)
+__device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t v, int l) {
+    return lane_id() == l ? v : old;
+}
+// number of lanes below this one in mask
+__device__ __forceinline__ uint32_t popc_lt(uint64_t mask) {
+    return (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}
+
 // GF(2) product a*b mod P in the reflected CRC-32 domain (zlib 1.2.12 multmodp).
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
     uint32_t p = 0;

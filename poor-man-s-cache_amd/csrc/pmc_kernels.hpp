@@ -34,6 +34,7 @@ struct DeflateArgs {
     uint64_t wave_bytes;  // per-wave working set bytes
     uint32_t *tokens;     // per-wave symbol slabs (kSlabSyms each)
     uint8_t *scratch;     // per-wave HBM working sets (HBM variant)
+    uint64_t *dbg;        // PMC_STAMPS builds: per-phase cycle sums (else unused)
 };
 
 struct InflateArgs {
@@ -53,10 +54,12 @@ struct InflateArgs {
 };
 
 uint64_t deflate_wave_bytes(bool hbm, uint64_t n);
+uint64_t deflate_small_wave_bytes(uint64_t n);
 uint64_t inflate_wave_bytes(bool hbm, uint64_t max_out, uint64_t max_in);
 
 template <bool kHbm>
 __global__ void deflate_kernel(DeflateArgs a);
+__global__ void deflate_small_kernel(DeflateArgs a);
 template <bool kHbm>
 __global__ void inflate_kernel(InflateArgs a);
 

@@ -15,7 +15,8 @@ from dataclasses import dataclass
 from typing import Optional
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpmc_codec.so")
+# PMC_LIB selects a diagnostic build (e.g. libpmc_codec_stamps.so); default is the product
+LIB_PATH = os.path.join(HERE, os.environ.get("PMC_LIB", "libpmc_codec.so"))
 DROPIN_PATH = os.path.join(HERE, "libgzip_dropin.so")
 
 CHUNK_SIZE = 16384
@@ -60,6 +61,7 @@ SIGNATURES = {
     "pmc_fill_layout": (_c.c_int, [_p, _p, _p, _u32, _u64, _u32, _u32, _p]),
     "pmc_compare_values": (_c.c_int, [_p, _p, _p, _p, _p, _p, _u32, _p, _p]),
     "pmc_route_keys": (_c.c_int, [_u64, _u32, _u32, _u32, _p, _p]),
+    "pmc_debug_stamps": (_c.c_int, [_p, _p]),
 }
 
 

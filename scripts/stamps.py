@@ -1,0 +1,49 @@
+"""Diagnostic: per-phase cycle shares of the deflate kernel (PMC_STAMPS build).
+
+PMC_LIB=libpmc_codec_stamps.so python scripts/stamps.py
+Prints wave-cycles per value for each phase.  Shares only -- never quoted as timings.
+"""
+import os
+import sys
+
+os.environ.setdefault("PMC_LIB", "libpmc_codec_stamps.so")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "poor-man-s-cache_amd")]
+
+import torch  # noqa: E402
+
+import pmc_codec  # noqa: E402
+from pmc_codec import device as D  # noqa: E402
+
+PHASES = ["stage+crc", "hash+sort", "parse", "huffman(lane0)", "emit", "trailer+copy", "-", "-"]
+
+
+def main():
+    ctx = pmc_codec.Context(0)
+    L = pmc_codec.lib()
+    d = os.path.join(ROOT, "tests", "golden", "data")
+    corpus_b = b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)))
+    corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).cuda()
+    dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
+    L.pmc_debug_stamps(ctx.handle, dbg.data_ptr())
+    for vlen, kind, n in ((1024, 0, 400_000), (256, 0, 400_000), (4096, 0, 100_000), (1024, 1, 200_000)):
+        data = torch.empty(n * vlen + 16, dtype=torch.uint8, device="cuda")
+        L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), 0x5EED if kind == 0 else 0xA1B2, kind, 0, None, n,
+                         vlen, data.data_ptr(), D.stream_handle())
+        off = torch.arange(n, dtype=torch.int64, device="cuda") * vlen
+        lens = torch.full((n,), vlen, dtype=torch.int32, device="cuda")
+        dbg.zero_()
+        torch.cuda.synchronize()
+        out, rc = D.compress(ctx, D.Batch(data, off, lens, n, vlen))
+        torch.cuda.synchronize()
+        s = dbg.cpu().tolist()
+        tot = sum(s)
+        print(f"vlen={vlen} kind={kind} n={n}: wave-cycles/value total {tot / n:,.0f}  rc!=0: {int((rc != 0).sum())}")
+        for k, name in enumerate(PHASES):
+            if s[k]:
+                print(f"   {name:16s} {s[k] / n:12,.0f}  {100 * s[k] / tot:5.1f}%")
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

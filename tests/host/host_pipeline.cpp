@@ -7,7 +7,9 @@
 // diffs the result against the golden vectors, so the device-side Huffman/emit code is
 // pinned on a CPU before any GPU run.
 //
-// usage: host_pipeline <in> <out>   (writes the gzip member of <in> to <out>)
+// usage: host_pipeline <in> <out> [v2]   (writes the gzip member of <in> to <out>; v2 =
+//        pmc_deflate_small.hip's Huffman formulation: packed-key heap, lengths from node
+//        depths, closed-form per-run scan_tree/send_tree, serial fallback on overflow)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -35,6 +37,135 @@ struct Bitbuf {
     }
 };
 
+// ---- v2 (pmc_deflate_small.hip) algorithms, serial form -----------------------------------
+// build_tree with heap entries (freq<<5|depth)<<10|node and a one-compare `smaller`, code
+// lengths = node depths, canonical codes; returns overflow instead of fixing it.
+struct V2Tree {
+    int max_code;
+    int64_t opt, stat;
+    bool overflow;
+    std::vector<uint32_t> code; // bitrev code | len << 16
+};
+static V2Tree v2_build(std::vector<uint32_t> freq, int elems, const CtData *stree, const uint8_t *extra, int base,
+                       int max_length) {
+    V2Tree t{};
+    std::vector<uint32_t> heap(1);
+    int max_code = -1;
+    for (int s = 0; s < elems; s++)
+        if (freq[s]) heap.push_back(((freq[s] << 5) << 10) | s), max_code = s;
+    int64_t opt = 0, stat = 0;
+    while (heap.size() - 1 < 2) {
+        int node = max_code < 2 ? ++max_code : 0;
+        heap.push_back(((1u << 5) << 10) | node);
+        freq[node] = 1;
+        opt -= 1;
+        if (stree) stat -= stree[node].dl;
+    }
+    int heap_len = (int)heap.size() - 1;
+    auto down = [&](int k) {
+        uint32_t v = heap[k];
+        int j = k << 1;
+        while (j <= heap_len) {
+            if (j < heap_len && (heap[j + 1] >> 10) <= (heap[j] >> 10)) j++;
+            if ((v >> 10) <= (heap[j] >> 10)) break;
+            heap[k] = heap[j];
+            k = j;
+            j <<= 1;
+        }
+        heap[k] = v;
+    };
+    for (int n = heap_len / 2; n >= 1; n--) down(n);
+    std::vector<int> dad(2 * elems + 2, -1);
+    int node = elems;
+    do {
+        uint32_t n = heap[1];
+        heap[1] = heap[heap_len--];
+        down(1);
+        uint32_t m = heap[1];
+        uint32_t kn = n >> 10, km = m >> 10, dn = kn & 31, dm = km & 31;
+        uint32_t d = (dn >= dm ? dn : dm) + 1;
+        dad[n & 1023] = dad[m & 1023] = node;
+        heap[1] = (((((kn >> 5) + (km >> 5)) << 5) | d) << 10) | node;
+        node++;
+        down(1);
+    } while (heap_len >= 2);
+    std::vector<uint32_t> len(elems, 0);
+    bool over = false;
+    int64_t po = 0, ps = 0;
+    for (int s = 0; s <= max_code; s++) {
+        if (!freq[s]) continue;
+        uint32_t d = 0;
+        for (int x = s; dad[x] >= 0; x = dad[x]) d++;
+        len[s] = d;
+        over |= d > (uint32_t)max_length;
+        uint32_t xb = s >= base ? extra[s - base] : 0;
+        po += (int64_t)freq[s] * (d + xb);
+        if (stree) ps += (int64_t)freq[s] * (stree[s].dl + xb);
+    }
+    t.overflow = over;
+    t.opt = opt + po;
+    t.stat = stat + ps;
+    t.max_code = max_code;
+    uint32_t bl_count[16] = {}, next_code[16] = {}, code = 0;
+    for (int s = 0; s <= max_code; s++) bl_count[len[s]]++;
+    bl_count[0] = 0;
+    for (int L = 1; L <= 15; L++) {
+        code = (code + bl_count[L - 1]) << 1;
+        next_code[L] = code;
+    }
+    t.code.assign(elems, 0);
+    for (int s = 0; s <= max_code; s++) {
+        uint32_t L = len[s];
+        if (!L) continue;
+        uint32_t c = next_code[L]++, r = 0;
+        for (uint32_t k = 0; k < L; k++) r = (r << 1) | ((c >> k) & 1);
+        t.code[s] = r | (L << 16);
+    }
+    return t;
+}
+// closed-form scan_tree / send_tree of one maximal run (v, R)
+template <class F>
+static void v2_run(uint32_t v, uint32_t R, F put) {
+    if (v) {
+        uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = rem / 6, last = rem % 6;
+        if (c1 < 4) {
+            for (uint32_t k = 0; k < c1; k++) put(v, 0, 0);
+        } else {
+            put(v, 0, 0);
+            put(16, c1 - 4, 2);
+        }
+        for (uint32_t k = 0; k < full; k++) put(16, 3, 2);
+        if (last) {
+            if (last < 3)
+                for (uint32_t k = 0; k < last; k++) put(v, 0, 0);
+            else
+                put(16, last - 3, 2);
+        }
+    } else {
+        uint32_t full = R / 138, last = R % 138;
+        for (uint32_t k = 0; k < full; k++) put(18, 127, 7);
+        if (last) {
+            if (last < 3)
+                for (uint32_t k = 0; k < last; k++) put(0, 0, 0);
+            else if (last <= 10)
+                put(17, last - 3, 3);
+            else
+                put(18, last - 11, 7);
+        }
+    }
+}
+template <class F>
+static void v2_runs(const std::vector<uint32_t> &code, int max_code, F on_run) {
+    int s = 0;
+    while (s <= max_code) {
+        uint32_t v = code[s] >> 16;
+        int e = s + 1;
+        while (e <= max_code && (code[e] >> 16) == v) e++;
+        on_run(v, (uint32_t)(e - s));
+        s = e;
+    }
+}
+
 static uint32_t crc32(const uint8_t *p, size_t n) {
     uint32_t c = 0xFFFFFFFFu;
     for (size_t i = 0; i < n; i++) {
@@ -45,7 +176,8 @@ static uint32_t crc32(const uint8_t *p, size_t n) {
 }
 
 int main(int argc, char **argv) {
-    if (argc != 3) return 2;
+    if (argc != 3 && argc != 4) return 2;
+    const bool use_v2 = argc == 4 && strcmp(argv[3], "v2") == 0;
     FILE *f = fopen(argv[1], "rb");
     std::vector<uint8_t> in;
     int ch;
@@ -100,7 +232,76 @@ int main(int argc, char **argv) {
     init_block(*tr);
     std::vector<uint32_t> tok;
     uint64_t block_start = 0, B = 0, wend = 0, i = 0;
+    auto flush_v2 = [&](uint64_t end, bool last) -> bool {
+        std::vector<uint32_t> lf(286), df(30), blf(19, 0);
+        for (int s = 0; s < 286; s++) lf[s] = tr->ltree[s].fc;
+        for (int s = 0; s < 30; s++) df[s] = tr->dtree[s].fc;
+        V2Tree tl = v2_build(lf, 286, T.static_ltree, T.extra_lbits, 257, 15);
+        V2Tree td = v2_build(df, 30, T.static_dtree, T.extra_dbits, 0, 15);
+        if (tl.overflow || td.overflow) return false;
+        auto count = [&](uint32_t v, uint32_t R) { v2_run(v, R, [&](uint32_t c, uint32_t, uint32_t) { blf[c]++; }); };
+        v2_runs(tl.code, tl.max_code, count);
+        v2_runs(td.code, td.max_code, count);
+        V2Tree tb = v2_build(blf, 19, nullptr, T.extra_blbits, 0, 7);
+        if (tb.overflow) return false;
+        int mbi;
+        for (mbi = 18; mbi >= 3; mbi--)
+            if ((tb.code[T.bl_order[mbi]] >> 16) != 0) break;
+        int64_t opt = tl.opt + td.opt + tb.opt + 3 * ((int64_t)mbi + 1) + 14, stat = tl.stat + td.stat;
+        uint64_t optb = ((uint64_t)opt + 10) >> 3, statb = ((uint64_t)stat + 10) >> 3;
+        if (statb <= optb) optb = statb;
+        uint64_t stored_len = end - block_start;
+        if (stored_len + 4 <= optb && block_start >= B) {
+            bb.put((0u << 1) + last, 3);
+            bb.pos = (bb.pos + 7) & ~7ull;
+            bb.put((unsigned)stored_len & 0xffff, 16);
+            bb.put((~(unsigned)stored_len) & 0xffff, 16);
+            for (uint64_t k = 0; k < stored_len; k++) bb.put(b[block_start + k], 8);
+        } else {
+            bool fixed = statb == optb;
+            std::vector<uint32_t> lc(288), dc(32);
+            for (int s = 0; s < 286; s++)
+                lc[s] = fixed ? (T.static_ltree[s].fc | (uint32_t)T.static_ltree[s].dl << 16) : tl.code[s];
+            for (int s = 0; s < 30; s++)
+                dc[s] = fixed ? (T.static_dtree[s].fc | (uint32_t)T.static_dtree[s].dl << 16) : td.code[s];
+            bb.put(((fixed ? 1u : 2u) << 1) + last, 3);
+            if (!fixed) {
+                bb.put(tl.max_code + 1 - 257, 5);
+                bb.put(td.max_code + 1 - 1, 5);
+                bb.put(mbi + 1 - 4, 4);
+                for (int k = 0; k <= mbi; k++) bb.put(tb.code[T.bl_order[k]] >> 16, 3);
+                auto send = [&](uint32_t v, uint32_t R) {
+                    v2_run(v, R, [&](uint32_t c, uint32_t xv, uint32_t xn) {
+                        bb.put(tb.code[c] & 0xffff, tb.code[c] >> 16);
+                        bb.put(xv, xn);
+                    });
+                };
+                v2_runs(tl.code, tl.max_code, send);
+                v2_runs(td.code, td.max_code, send);
+            }
+            for (uint32_t t : tok) {
+                uint32_t dist = t >> 16, l8 = t & 0xff;
+                if (!dist) {
+                    bb.put(lc[l8] & 0xffff, lc[l8] >> 16);
+                } else {
+                    uint32_t code = T.length_code[l8];
+                    bb.put(lc[code + 257] & 0xffff, lc[code + 257] >> 16);
+                    bb.put((l8 - T.base_length[code]) & ((1u << T.extra_lbits[code]) - 1), T.extra_lbits[code]);
+                    uint32_t dm = dist - 1, dcd = d_code(T, dm);
+                    bb.put(dc[dcd] & 0xffff, dc[dcd] >> 16);
+                    bb.put((dm - T.base_dist[dcd]) & ((1u << T.extra_dbits[dcd]) - 1), T.extra_dbits[dcd]);
+                }
+            }
+            bb.put(lc[256] & 0xffff, lc[256] >> 16);
+            if (last) bb.pos = (bb.pos + 7) & ~7ull;
+        }
+        init_block(*tr);
+        tok.clear();
+        block_start = end;
+        return true;
+    };
     auto flush = [&](uint64_t end, bool last) {
+        if (use_v2 && flush_v2(end, last)) return;
         BlockPlan p = plan_block(*tr, T);
         uint64_t stored_len = end - block_start;
         if (stored_len + 4 <= p.opt_lenb && block_start >= B) {

@@ -50,7 +50,11 @@ def test_compress_all_golden_vectors(ctx, D, golden):
     rc = rc.cpu().numpy()
     got = out.host_items()
     bad = [k for k, (r, g) in enumerate(pairs) if rc[k] != 0 or got[k] != g]
-    assert not bad, f"{len(bad)} vectors differ; first {bad[:8]} sizes {[len(pairs[k][0]) for k in bad[:8]]}"
+    if bad:
+        from deflate_dissect import explain
+        detail = "\n".join(f"  #{k} ({len(pairs[k][0])} B, rc {rc[k]}): {explain(got[k], pairs[k][1])}"
+                           for k in bad[:12])
+        raise AssertionError(f"{len(bad)} of {len(pairs)} vectors differ:\n{detail}")
 
 
 def test_decompress_all_golden_vectors(ctx, D, golden):

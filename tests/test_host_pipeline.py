@@ -18,14 +18,17 @@ def host_bin():
     return exe, d
 
 
-def test_host_pipeline_matches_goldens(golden, host_bin):
+@pytest.mark.parametrize("mode", ["v1", "v2"])
+def test_host_pipeline_matches_goldens(golden, host_bin, mode):
+    """v1: pmc_trees.hpp as the general kernel runs it; v2: the small kernel's formulation
+    (packed-key heap, depth lengths, closed-form per-run scan_tree/send_tree)."""
     exe, d = host_bin
     src, dst = os.path.join(d, "in"), os.path.join(d, "out")
     bad = []
     for k, (r, g) in enumerate(golden.pairs()):
         with open(src, "wb") as f:
             f.write(r)
-        subprocess.check_call([exe, src, dst])
+        subprocess.check_call([exe, src, dst] + (["v2"] if mode == "v2" else []))
         with open(dst, "rb") as f:
             if f.read() != g:
                 bad.append(k)
