@@ -118,7 +118,7 @@ int pmc_route_keys(uint64_t first, uint32_t n, uint32_t num_shards, uint32_t n_g
                    void *stream);
 
 /* Diagnostics: in a library built with -DPMC_STAMPS, deflate kernels add per-phase cycle
- * sums (8 x uint64, device memory) into dev_buf; NULL disables.  No effect otherwise. */
+ * sums (16 x uint64, device memory) into dev_buf; NULL disables.  No effect otherwise. */
 int pmc_debug_stamps(pmc_ctx *ctx, uint64_t *dev_buf);
 
 #ifdef __cplusplus

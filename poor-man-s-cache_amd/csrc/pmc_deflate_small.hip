@@ -124,6 +124,50 @@ struct RegHeap {
     }
 };
 
+// Small heaps (the common case): one VGPR holds entries 0..63 (entry k in lane k); two
+// VGPRs hold entries 0..127 interleaved (entry k in lane k>>1 of h[k&1]) so the two
+// children 2k, 2k+1 of node k sit in lane k of h0 and h1 -- one readlane each, no select.
+template <int NR>
+struct RegHeapN {
+    uint32_t h0, h1;
+    __device__ uint32_t get(int k) const {
+        if (NR == 1) return readlane(h0, k & 63);
+        return readlane((k & 1) ? h1 : h0, (k >> 1) & 63);
+    }
+    __device__ void set(int k, uint32_t v) {
+        if (NR == 1) {
+            h0 = writelane(h0, v, k);
+        } else if (k & 1) {
+            h1 = writelane(h1, v, k >> 1);
+        } else {
+            h0 = writelane(h0, v, k >> 1);
+        }
+    }
+    __device__ void down(int k, int heap_len) {
+        uint32_t v = get(k);
+        int j = k << 1;
+        while (j <= heap_len) {
+            uint32_t x, y;
+            if (NR == 1) {
+                x = readlane(h0, j & 63);
+                y = readlane(h0, (j + 1) & 63);
+            } else {
+                x = readlane(h0, k & 63);
+                y = readlane(h1, k & 63);
+            }
+            if (j < heap_len && (y >> 10) <= (x >> 10)) {
+                j++;
+                x = y;
+            }
+            if ((v >> 10) <= (x >> 10)) break;
+            set(k, x);
+            k = j;
+            j <<= 1;
+        }
+        set(k, v);
+    }
+};
+
 struct TreeOut {
     int max_code;
     int64_t opt, stat;
@@ -148,7 +192,7 @@ struct SmallWave {
     uint32_t *tok;
     Trees *fb; // HBM scratch for the serial fallback
     const uint32_t *crc_tab;
-    uint64_t st[8];
+    uint64_t st[16];
     uint64_t t_last;
 
     __device__ void stamp(int k) {
@@ -275,6 +319,35 @@ struct SmallWave {
         return best > b0 ? best : 0u;
     }
 
+    // build_tree's heapify + merge loop (trees.c) on a register heap; returns the next
+    // node id (root = result - 1).  Father links go to dad[] (lane 0 stores).
+    template <class Heap>
+    __device__ int heap_merge(Heap &hp, int heap_len, int elems, bool &deep) {
+        const int l = lane_id();
+        for (int n = heap_len / 2; n >= 1; n--) hp.down(n, heap_len);
+        int node = elems;
+        do {
+            const uint32_t n = hp.get(1);
+            hp.set(1, hp.get(heap_len));
+            heap_len--;
+            hp.down(1, heap_len);
+            const uint32_t m = hp.get(1);
+            const uint32_t kn = n >> 10, km = m >> 10;
+            const uint32_t dn = kn & 31, dm = km & 31;
+            const uint32_t d = (dn >= dm ? dn : dm) + 1;
+            deep |= d >= 31;
+            const uint32_t key = (((kn >> 5) + (km >> 5)) << 5) | (d & 31);
+            if (l == 0) {
+                dad[n & 1023] = (uint16_t)node;
+                dad[m & 1023] = (uint16_t)node;
+            }
+            hp.set(1, (key << 10) | (uint32_t)node);
+            node++;
+            hp.down(1, heap_len);
+        } while (heap_len >= 2);
+        return node;
+    }
+
     // ---- Huffman: build_tree for one tree -------------------------------------------------
     // freq[0..elems) in LDS (u32).  Writes code_out[s] = bitrev code | len << 16 for
     // s <= max_code (0 for unused), returns zlib's opt_len/static_len contributions.
@@ -295,52 +368,61 @@ struct SmallWave {
         wave_sync();
         // dummies (build_tree: while (heap_len < 2))
         int64_t opt = 0, stat = 0;
-        to.dummy[0] = to.dummy[1] = -1;
-        while (heap_len < 2) {
-            const int node = max_code < 2 ? ++max_code : 0;
-            to.dummy[to.dummy[0] < 0 ? 0 : 1] = node;
-            if (l == 0) {
-                code_out[++heap_len] = ((1u << 5) << 10) | (uint32_t)node;
-                freq[node] = 1;
-            } else {
-                ++heap_len;
-            }
+        // (all control values stay wave-uniform -- only the LDS stores are lane-guarded --
+        //  so the heap loop below compiles to scalar control flow)
+        int d0 = -1, d1 = -1;
+        if (heap_len < 2) {
+            d0 = max_code < 2 ? ++max_code : 0;
             opt -= 1;
-            if (stree) stat -= stree[node].dl;
-        }
-        wave_sync();
-        RegHeap hp;
-        hp.h0 = code_out[l];
-        hp.h1 = code_out[64 + l];
-        hp.h2 = code_out[128 + l];
-        hp.h3 = code_out[192 + l];
-        hp.h4 = code_out[256 + l < 288 ? 256 + l : 287];
-        // 2. heapify + merge (all uniform scalar control; the heap never leaves VGPRs)
-        for (int n = heap_len / 2; n >= 1; n--) hp.down(n, heap_len);
-        int node = elems;
-        bool deep = false;
-        do {
-            const uint32_t n = hp.get(1);
-            hp.set(1, hp.get(heap_len));
-            heap_len--;
-            hp.down(1, heap_len);
-            const uint32_t m = hp.get(1);
-            const uint32_t kn = n >> 10, km = m >> 10;
-            const uint32_t dn = kn & 31, dm = km & 31;
-            const uint32_t d = (dn >= dm ? dn : dm) + 1;
-            deep |= d >= 31;
-            const uint32_t key = (((kn >> 5) + (km >> 5)) << 5) | (d & 31);
-            if (l == 0) {
-                dad[n & 1023] = (uint16_t)node;
-                dad[m & 1023] = (uint16_t)node;
+            if (stree) stat -= stree[d0].dl;
+            if (heap_len + 1 < 2) {
+                d1 = max_code < 2 ? ++max_code : 0;
+                opt -= 1;
+                if (stree) stat -= stree[d1].dl;
             }
-            hp.set(1, (key << 10) | (uint32_t)node);
-            node++;
-            hp.down(1, heap_len);
-        } while (heap_len >= 2);
+        }
+        to.dummy[0] = d0;
+        to.dummy[1] = d1;
+        if (l == 0) {
+            if (d0 >= 0) {
+                code_out[heap_len + 1] = ((1u << 5) << 10) | (uint32_t)d0;
+                freq[d0] = 1;
+            }
+            if (d1 >= 0) {
+                code_out[heap_len + 2] = ((1u << 5) << 10) | (uint32_t)d1;
+                freq[d1] = 1;
+            }
+        }
+        heap_len = rfl(heap_len + (d0 >= 0) + (d1 >= 0));
+        max_code = rfl(max_code);
+        wave_sync();
+        stamp(8);
+        // 2. heapify + merge (all uniform scalar control; the heap never leaves VGPRs)
+        int node;
+        bool deep = false;
+        if (heap_len < 64) {
+            RegHeapN<1> hp;
+            hp.h0 = code_out[l];
+            hp.h1 = 0;
+            node = heap_merge(hp, heap_len, elems, deep);
+        } else if (heap_len < 128) {
+            RegHeapN<2> hp;
+            hp.h0 = code_out[2 * l];
+            hp.h1 = code_out[2 * l + 1];
+            node = heap_merge(hp, heap_len, elems, deep);
+        } else {
+            RegHeap hp;
+            hp.h0 = code_out[l];
+            hp.h1 = code_out[64 + l];
+            hp.h2 = code_out[128 + l];
+            hp.h3 = code_out[192 + l];
+            hp.h4 = code_out[256 + l < 288 ? 256 + l : 287];
+            node = heap_merge(hp, heap_len, elems, deep);
+        }
         const int root = node - 1;
         if (l == 0) dad[root] = (uint16_t)root;
         wave_sync();
+        stamp(9);
         // 3. depth of every node by pointer jumping over the father links (depth <= 21)
         for (int x = l; x < node; x += 64) {
             bool in_tree = x >= elems || (x <= max_code && freq[x] != 0);
@@ -370,6 +452,7 @@ struct SmallWave {
             }
             wave_sync();
         }
+        stamp(10);
         // 4. code lengths, overflow check, opt_len / static_len sums
         uint32_t over = 0;
         int64_t po = 0, ps = 0;
@@ -389,6 +472,7 @@ struct SmallWave {
         to.stat = stat + ps;
         to.max_code = max_code;
         if (over) return to;
+        stamp(11);
         // 5. gen_codes: canonical code = next_code[len] + rank among equal lengths
         uint32_t bl_count[16];
 #pragma unroll
@@ -422,6 +506,7 @@ struct SmallWave {
                 code_out[s] = len ? ((__builtin_bitreverse32(mycode) >> (32 - len)) | (len << 16)) : 0u;
         }
         wave_sync();
+        stamp(12);
         return to;
     }
 
@@ -555,9 +640,10 @@ struct SmallWave {
         }
         if (l == 0) lfreq[kEndBlock] = 1;
         wave_sync();
-        stamp(2);
+        stamp(6);
         TreeOut tl = build_tree(lfreq, kLCodes, TT.static_ltree, TT.extra_lbits, kLiterals + 1, kMaxBits, lcode);
         TreeOut td = build_tree(dfreq, kDCodes, TT.static_dtree, TT.extra_dbits, 0, kMaxBits, dcode);
+        stamp(3);
         // (not in dad[]: the bit-length tree's build_tree below reuses dad[])
         uint16_t *runL = runs, *runD = runs + 288;
         TreeOut tb{};
@@ -613,7 +699,7 @@ struct SmallWave {
             opt_len = (int64_t)ol * 8 - 10;
             static_len = (int64_t)sl * 8 - 10;
         }
-        stamp(3);
+        stamp(7);
         const uint32_t opt_lenb_raw = (uint32_t)(((uint64_t)opt_len + 3 + 7) >> 3);
         const uint32_t static_lenb = (uint32_t)(((uint64_t)static_len + 3 + 7) >> 3);
         const uint32_t opt_lenb = static_lenb <= opt_lenb_raw ? static_lenb : opt_lenb_raw;
@@ -784,6 +870,7 @@ struct SmallWave {
         if (match_available) emit(b[i - 1]);
         if ((ntok & 63) != 0 && (uint32_t)l < (ntok & 63)) tok[(ntok & ~63u) + l] = treg;
         wave_sync_global();
+        stamp(2);
         // flush: the output image aliases the (dead) sort scratch
         for (uint64_t k = l; k < out_words; k += 64) outw[k] = 0;
         wave_sync();
@@ -850,7 +937,7 @@ __global__ void __launch_bounds__(256) deflate_small_kernel(DeflateArgs a) {
     w.tok = a.tokens + wave * kSlabSyms;
     w.fb = reinterpret_cast<Trees *>(a.scratch + wave * sizeof(Trees));
     w.crc_tab = crc_tab;
-    for (int k = 0; k < 8; k++) w.st[k] = 0;
+    for (int k = 0; k < 16; k++) w.st[k] = 0;
 #ifdef PMC_STAMPS
     w.t_last = __builtin_amdgcn_s_memtime();
 #endif
@@ -879,7 +966,7 @@ __global__ void __launch_bounds__(256) deflate_small_kernel(DeflateArgs a) {
     }
 #ifdef PMC_STAMPS
     if (l == 0 && a.dbg)
-        for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&a.dbg[k], (unsigned long long)w.st[k]);
+        for (int k = 0; k < 16; k++) atomicAdd((unsigned long long *)&a.dbg[k], (unsigned long long)w.st[k]);
 #endif
 }
 

@@ -15,7 +15,8 @@ import torch  # noqa: E402
 import pmc_codec  # noqa: E402
 from pmc_codec import device as D  # noqa: E402
 
-PHASES = ["stage+crc", "hash+sort", "parse", "huffman(lane0)", "emit", "trailer+copy", "-", "-"]
+PHASES = ["stage+crc", "hash+sort", "parse", "trees lit+dist (rest)", "emit", "trailer+copy", "zero+histogram",
+          "runs+bl tree (rest)", "bt:leaves", "bt:heap", "bt:depths", "bt:sums", "bt:codes", "-", "-", "-"]
 
 
 def main():
@@ -24,7 +25,7 @@ def main():
     d = os.path.join(ROOT, "tests", "golden", "data")
     corpus_b = b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)))
     corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).cuda()
-    dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
     L.pmc_debug_stamps(ctx.handle, dbg.data_ptr())
     for vlen, kind, n in ((1024, 0, 400_000), (256, 0, 400_000), (4096, 0, 100_000), (1024, 1, 200_000)):
         data = torch.empty(n * vlen + 16, dtype=torch.uint8, device="cuda")
