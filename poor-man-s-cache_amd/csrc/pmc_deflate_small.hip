@@ -175,23 +175,24 @@ struct TreeOut {
     int dummy[2]; // symbols whose freq build_tree set to 1 (zlib's "at least 2 codes"), or -1
 };
 
+#define PMC_GLB __attribute__((address_space(1)))
 struct SmallWave {
-    uint8_t *b;
-    uint32_t *bw;
-    uint16_t *S, *R;
-    uint32_t *lfreq, *dfreq, *blfreq;
-    uint8_t *W;
-    uint32_t *outw;
-    uint8_t *outb;
-    uint64_t out_words;
-    uint32_t *lcode, *dcode, *blcode;
-    uint16_t *dad;
-    uint8_t *dep;
-    uint16_t *runs;
-    uint16_t *T, *H, *cnt;
-    uint32_t *tok;
+    // every working array is LDS-typed (ds_* with 32-bit addresses)
+    PMC_LDS uint8_t *b;
+    PMC_LDS uint32_t *bw;
+    PMC_LDS uint16_t *S, *R;
+    PMC_LDS uint32_t *lfreq, *dfreq, *blfreq;
+    PMC_LDS uint32_t *outw;
+    PMC_LDS uint8_t *outb;
+    uint32_t out_words;
+    PMC_LDS uint32_t *lcode, *dcode, *blcode;
+    PMC_LDS uint16_t *dad;
+    PMC_LDS uint8_t *dep;
+    PMC_LDS uint16_t *runs;
+    PMC_LDS uint16_t *T, *H, *cnt;
+    PMC_GLB uint32_t *tok;
     Trees *fb; // HBM scratch for the serial fallback
-    const uint32_t *crc_tab;
+    PMC_LDS const uint32_t *crc_tab;
     uint64_t st[16];
     uint64_t t_last;
 
@@ -217,8 +218,8 @@ struct SmallWave {
         wave_sync();
         for (int pass = 0; pass < 4; pass++) {
             const int sh = 4 * pass;
-            const uint16_t *src = pass == 0 ? nullptr : (pass & 1 ? T : S);
-            uint16_t *dst = pass & 1 ? S : T;
+            PMC_LDS const uint16_t *src = pass == 0 ? nullptr : (pass & 1 ? T : S);
+            PMC_LDS uint16_t *dst = pass & 1 ? S : T;
             for (int d = 0; d < 16; d++) cnt[d * 64 + l] = 0;
             wave_sync();
             for (uint32_t j = 0; j < c; j++) {
@@ -351,8 +352,9 @@ struct SmallWave {
     // ---- Huffman: build_tree for one tree -------------------------------------------------
     // freq[0..elems) in LDS (u32).  Writes code_out[s] = bitrev code | len << 16 for
     // s <= max_code (0 for unused), returns zlib's opt_len/static_len contributions.
-    __device__ __noinline__ TreeOut build_tree(uint32_t *freq, int elems, const CtData *stree, const uint8_t *extra,
-                                  int extra_base, int max_length, uint32_t *code_out) {
+    __device__ __noinline__ TreeOut build_tree(PMC_LDS uint32_t *freq, int elems, const CtData *stree,
+                                               const uint8_t *extra, int extra_base, int max_length,
+                                               PMC_LDS uint32_t *code_out) {
         const int l = lane_id();
         TreeOut to{};
         // 1. leaves in symbol order -> staging (code_out reused) at heap index 1..k
@@ -511,20 +513,20 @@ struct SmallWave {
     }
 
     // per maximal run of code lengths (value v, length R): bl-code counts (scan_tree)
-    __device__ static void run_counts(uint32_t v, uint32_t R, uint32_t *blfreq) {
+    __device__ static void run_counts(uint32_t v, uint32_t R, PMC_LDS uint32_t *blfreq) {
         if (v) {
             uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = rem / 6, last = rem % 6;
             uint32_t nv = (c1 < 4 ? c1 : 1) + (last < 3 ? last : 0);
             uint32_t n16 = (c1 >= 4 ? 1 : 0) + full + (last >= 3 ? 1 : 0);
-            if (nv) atomicAdd(&blfreq[v], nv);
-            if (n16) atomicAdd(&blfreq[16], n16);
+            if (nv) lds_add(&blfreq[v], nv);
+            if (n16) lds_add(&blfreq[16], n16);
         } else {
             uint32_t full = R / 138, last = R % 138;
             uint32_t n18 = full + (last > 10 ? 1 : 0), n17 = (last >= 3 && last <= 10) ? 1 : 0;
             uint32_t n0 = last < 3 ? last : 0;
-            if (n0) atomicAdd(&blfreq[0], n0);
-            if (n17) atomicAdd(&blfreq[17], n17);
-            if (n18) atomicAdd(&blfreq[18], n18);
+            if (n0) lds_add(&blfreq[0], n0);
+            if (n17) lds_add(&blfreq[17], n17);
+            if (n18) lds_add(&blfreq[18], n18);
         }
     }
     // bits of one run (send_tree); emit into the image at pos when out != nullptr
@@ -576,15 +578,15 @@ struct SmallWave {
         uint32_t lo = (uint32_t)(v << s);
         uint32_t mid = (uint32_t)(s ? (v >> (32 - s)) : (v >> 32));
         uint32_t hi = s ? (uint32_t)(v >> (64 - s)) : 0u;
-        if (lo) atomicOr(&outw[w], lo);
-        if (n + s > 32 && mid) atomicOr(&outw[w + 1], mid);
-        if (n + s > 64 && hi) atomicOr(&outw[w + 2], hi);
+        if (lo) lds_or(&outw[w], lo);
+        if (n + s > 32 && mid) lds_or(&outw[w + 1], mid);
+        if (n + s > 64 && hi) lds_or(&outw[w + 2], hi);
     }
 
     // scan_tree for lengths code[0..max_code]: records run lengths at run starts into
     // runR (u16) and adds the bl counts.  Chunks are walked back to front so each run
     // start knows where the next run begins.
-    __device__ void scan_runs(const uint32_t *code, int max_code, uint16_t *runR) {
+    __device__ void scan_runs(PMC_LDS const uint32_t *code, int max_code, PMC_LDS uint16_t *runR) {
         const int l = lane_id();
         int next_start = max_code + 1;
         for (int c0 = (max_code / 64) * 64; c0 >= 0; c0 -= 64) {
@@ -604,7 +606,8 @@ struct SmallWave {
         }
     }
     // send_tree: every run start writes its symbols at its prefix offset; returns bits
-    __device__ uint64_t send_runs(const uint32_t *code, int max_code, const uint16_t *runR, uint64_t pos) {
+    __device__ uint64_t send_runs(PMC_LDS const uint32_t *code, int max_code, PMC_LDS const uint16_t *runR,
+                                  uint64_t pos) {
         const int l = lane_id();
         uint64_t base = pos;
         for (int c0 = 0; c0 <= max_code; c0 += 64) {
@@ -632,10 +635,10 @@ struct SmallWave {
         for (uint32_t t = l; t < ntok; t += 64) {
             const uint32_t tk = tok[t], dist = tk >> 16, lc = tk & 0xff;
             if (dist == 0) {
-                atomicAdd(&lfreq[lc], 1u);
+                lds_add(&lfreq[lc], 1u);
             } else {
-                atomicAdd(&lfreq[TT.length_code[lc] + kLiterals + 1], 1u);
-                atomicAdd(&dfreq[d_code(TT, dist - 1)], 1u);
+                lds_add(&lfreq[TT.length_code[lc] + kLiterals + 1], 1u);
+                lds_add(&dfreq[d_code(TT, dist - 1)], 1u);
             }
         }
         if (l == 0) lfreq[kEndBlock] = 1;
@@ -645,7 +648,7 @@ struct SmallWave {
         TreeOut td = build_tree(dfreq, kDCodes, TT.static_dtree, TT.extra_dbits, 0, kMaxBits, dcode);
         stamp(3);
         // (not in dad[]: the bit-length tree's build_tree below reuses dad[])
-        uint16_t *runL = runs, *runD = runs + 288;
+        PMC_LDS uint16_t *runL = runs, *runD = runs + 288;
         TreeOut tb{};
         int mbi = 0;
         bool fallback = tl.overflow || td.overflow;
@@ -798,7 +801,7 @@ struct SmallWave {
 
     // bit sink for the serial fallback's send_all_trees (lane 0)
     struct LaneBitsL {
-        uint32_t *out;
+        PMC_LDS uint32_t *out;
         uint64_t pos;
         __device__ void put(unsigned v, int n) {
             if (n == 0) return;
@@ -913,30 +916,30 @@ __global__ void __launch_bounds__(256) deflate_small_kernel(DeflateArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     uint8_t *base = lds + 1024 + (uint64_t)wib * a.wave_bytes;
     const SmallLayout L = small_layout(a.cap_len);
+    uint8_t *W = base + L.W;
     SmallWave w;
-    w.b = base + L.bytes;
-    w.bw = reinterpret_cast<uint32_t *>(base + L.bytes);
-    w.S = reinterpret_cast<uint16_t *>(base + L.S);
-    w.R = reinterpret_cast<uint16_t *>(base + L.R);
-    w.lfreq = reinterpret_cast<uint32_t *>(base + L.freq);
+    w.b = to_lds<uint8_t>(base + L.bytes);
+    w.bw = to_lds<uint32_t>(base + L.bytes);
+    w.S = to_lds<uint16_t>(base + L.S);
+    w.R = to_lds<uint16_t>(base + L.R);
+    w.lfreq = to_lds<uint32_t>(base + L.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;
-    w.W = base + L.W;
-    w.outw = reinterpret_cast<uint32_t *>(w.W + L.out);
-    w.outb = w.W + L.out;
-    w.out_words = L.out_words;
-    w.lcode = reinterpret_cast<uint32_t *>(w.W + L.lcode);
-    w.dcode = reinterpret_cast<uint32_t *>(w.W + L.dcode);
-    w.blcode = reinterpret_cast<uint32_t *>(w.W + L.blcode);
-    w.dad = reinterpret_cast<uint16_t *>(w.W + L.dad);
-    w.dep = w.W + L.dep;
-    w.runs = reinterpret_cast<uint16_t *>(w.W + L.runs);
-    w.T = reinterpret_cast<uint16_t *>(w.W + L.T);
-    w.H = reinterpret_cast<uint16_t *>(w.W + L.H);
-    w.cnt = reinterpret_cast<uint16_t *>(w.W + L.cnt);
-    w.tok = a.tokens + wave * kSlabSyms;
+    w.outw = to_lds<uint32_t>(W + L.out);
+    w.outb = to_lds<uint8_t>(W + L.out);
+    w.out_words = (uint32_t)L.out_words;
+    w.lcode = to_lds<uint32_t>(W + L.lcode);
+    w.dcode = to_lds<uint32_t>(W + L.dcode);
+    w.blcode = to_lds<uint32_t>(W + L.blcode);
+    w.dad = to_lds<uint16_t>(W + L.dad);
+    w.dep = to_lds<uint8_t>(W + L.dep);
+    w.runs = to_lds<uint16_t>(W + L.runs);
+    w.T = to_lds<uint16_t>(W + L.T);
+    w.H = to_lds<uint16_t>(W + L.H);
+    w.cnt = to_lds<uint16_t>(W + L.cnt);
+    w.tok = (PMC_GLB uint32_t *)(a.tokens + wave * kSlabSyms);
     w.fb = reinterpret_cast<Trees *>(a.scratch + wave * sizeof(Trees));
-    w.crc_tab = crc_tab;
+    w.crc_tab = to_lds<const uint32_t>(crc_tab);
     for (int k = 0; k < 16; k++) w.st[k] = 0;
 #ifdef PMC_STAMPS
     w.t_last = __builtin_amdgcn_s_memtime();

@@ -12,6 +12,20 @@
 namespace pmc {
 
 constexpr int kWave = 64;
+
+// LDS-typed pointers: accesses compile to ds_* with 32-bit addresses wherever the pointer
+// itself lives (a generic pointer kept in a struct in scratch degrades to flat_* ops).
+#define PMC_LDS __attribute__((address_space(3)))
+template <class T>
+__device__ __forceinline__ PMC_LDS T *to_lds(void *p) {
+    return (PMC_LDS T *)(p);
+}
+__device__ __forceinline__ uint32_t lds_add(PMC_LDS uint32_t *p, uint32_t v) {
+    return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
+}
+__device__ __forceinline__ uint32_t lds_or(PMC_LDS uint32_t *p, uint32_t v) {
+    return __atomic_fetch_or(p, v, __ATOMIC_RELAXED);
+}
 constexpr uint32_t kCrcPoly = 0xEDB88320u;
 constexpr int kCrcShiftEntries = 4096; // x^(128*d) mod P for d < 4096 (16-byte steps)
 
@@ -142,8 +156,8 @@ __device__ __forceinline__ uint32_t crc_shift_chunks(uint32_t d) {
 // chunk holding byte 0) is shifted past the d*16 bytes that follow it by one GF(2)
 // multiply with x^(128 d) mod P, and the wave XOR-reduces.  By linearity of the CRC
 // register this equals the serial crc32().  `tab` is a 256-entry table (LDS).
-template <class BytePtr>
-__device__ inline uint32_t wave_crc32(BytePtr buf, uint32_t len, const uint32_t *tab) {
+template <class BytePtr, class TabPtr>
+__device__ inline uint32_t wave_crc32(BytePtr buf, uint32_t len, TabPtr tab) {
     uint32_t nchunks = (len + 15) >> 4;
     uint32_t acc = 0;
     for (uint32_t d = (uint32_t)lane_id(); d < nchunks; d += 64) {
