@@ -28,6 +28,36 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 META_BYTES = 12        # +12 B offset/len per value per direction
 
 
+NUM_SHARDS = 128       # .env:4 as deployed; server.cpp:113 routes hash % NUM_SHARDS
+
+
+def route_span(n, world):
+    """Keys "key"+0 .. span-1 are routed; every rank finds >= n of its own among them."""
+    return int(n * world * 1.05) + 4096
+
+
+def select_rank_keys(route, rank, n):
+    """Global indices of the first n keys whose routed GPU (route[i], any torch device) is
+    `rank` -- the rank's weak-scaling share of the key space."""
+    import torch
+    idx = torch.nonzero(route == rank).flatten()[:n].to(torch.int64).contiguous()
+    if idx.numel() != n:
+        raise RuntimeError(f"rank {rank}: only {idx.numel()} of {n} keys routed in the span")
+    return idx
+
+
+def reduce_over_ranks(times, sums, world, device):
+    """Max over ranks of the step times, sum over ranks of the byte / error counters."""
+    import torch
+    t = torch.tensor(times, dtype=torch.float64, device=device)
+    a = torch.tensor(sums, dtype=torch.float64, device=device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(a, op=dist.ReduceOp.SUM)
+    return [float(x) for x in t.tolist()], [float(x) for x in a.tolist()]
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,11 +154,10 @@ def main():
     sh = stream.cuda_stream
     # ---- this rank's keys: route "key"+i to GPUs, take the first n routed here -----------
     if world > 1:
-        span = int(n * world * 1.05) + 4096
+        span = route_span(n, world)
         route = torch.empty(span, dtype=torch.uint8, device=dev)
-        assert L.pmc_route_keys(0, span, 128, world, route.data_ptr(), sh) == 0
-        index = torch.nonzero(route == rank).flatten()[:n].to(torch.int64).contiguous()
-        assert index.numel() == n
+        assert L.pmc_route_keys(0, span, NUM_SHARDS, world, route.data_ptr(), sh) == 0
+        index = select_rank_keys(route, rank, n)
         del route
         idx_ptr = index.data_ptr()
     else:
@@ -187,13 +216,8 @@ def main():
     bad = int(mism.item()) + int((crc != 0).sum().item()) + int((brc != 0).sum().item())
     comp_bytes = int(clen.to(torch.int64).sum().item())
 
-    t_step = torch.tensor([wall / args.steps, tc, td], dtype=torch.float64, device=dev)
-    agg = torch.tensor([float(n * vlen), float(comp_bytes), float(bad)], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t_step, op=dist.ReduceOp.MAX)
-        dist.all_reduce(agg, op=dist.ReduceOp.SUM)
-    t_step_s, tc_max, td_max = (float(x) for x in t_step.tolist())
-    total_bytes, total_comp, total_bad = (float(x) for x in agg.tolist())
+    (t_step_s, tc_max, td_max), (total_bytes, total_comp, total_bad) = reduce_over_ranks(
+        [wall / args.steps, tc, td], [float(n * vlen), float(comp_bytes), float(bad)], world, dev)
 
     h2h = None
     if args.h2h and world == 1:
@@ -228,7 +252,7 @@ def main():
                        "parallelism": f"shard-partitioned x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "pmc::deflate_kernel<false>",
+                         "kernel": "pmc::deflate_small_kernel",
                          "alg_bytes_per_launch": alg_c, "avg_launch_ms": tc * 1e3},
             "cpu_baseline": cpu,
             "compress_gib_s": gib / world / tc_max, "decompress_gib_s": gib / world / td_max,
