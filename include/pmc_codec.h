@@ -117,8 +117,9 @@ int pmc_compare_values(const uint8_t *a, const uint64_t *a_off, const uint8_t *b
 int pmc_route_keys(uint64_t first, uint32_t n, uint32_t num_shards, uint32_t n_gpus, uint8_t *gpu,
                    void *stream);
 
-/* Diagnostics: in a library built with -DPMC_STAMPS, deflate kernels add per-phase cycle
- * sums (16 x uint64, device memory) into dev_buf; NULL disables.  No effect otherwise. */
+/* Diagnostics: in a library built with -DPMC_STAMPS, the kernels add per-phase cycle sums
+ * into dev_buf (32 x uint64, device memory: [0,16) deflate, [16,32) inflate); NULL disables.
+ * No effect otherwise. */
 int pmc_debug_stamps(pmc_ctx *ctx, uint64_t *dev_buf);
 
 #ifdef __cplusplus

@@ -351,7 +351,7 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
     hipStream_t st = (hipStream_t)stream;
-    InflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr};
+    InflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, ctx->dbg ? ctx->dbg + 16 : nullptr};
     // output image capacity for the LDS kernel; the compressed input of a member whose
     // output fits is at most gzip_bound(out) unless it is not a deflate member at all
     uint64_t out_cap = std::min<uint64_t>(inflate_lds_out_limit(), std::max<uint64_t>(max_len, 1));
@@ -555,7 +555,7 @@ PMC_API int pmc_route_keys(uint64_t first, uint32_t n, uint32_t num_shards, uint
     return hipGetLastError() == hipSuccess ? PMC_OK : PMC_E_NO_DEVICE;
 }
 
-// Diagnostics: device buffer of 8 uint64 that PMC_STAMPS builds add per-phase cycles into.
+// Diagnostics: device buffer of 32 uint64 that PMC_STAMPS builds add per-phase cycles into.
 PMC_API int pmc_debug_stamps(pmc_ctx *ctx, uint64_t *dev_buf) {
     if (!ctx) return PMC_E_ARG;
     ctx->dbg = dev_buf;

@@ -190,6 +190,7 @@ struct SmallWave {
     PMC_LDS uint8_t *dep;
     PMC_LDS uint16_t *runs;
     PMC_LDS uint16_t *T, *H, *cnt;
+    PMC_LDS uint32_t *M; // per-position match_all results (aliases T/H after the sort)
     PMC_GLB uint32_t *tok;
     Trees *fb; // HBM scratch for the serial fallback
     PMC_LDS const uint32_t *crc_tab;
@@ -260,17 +261,91 @@ struct SmallWave {
         wave_sync();
     }
 
+    // 8 bytes at p (dword-aligned LDS reads + alignbyte; the value is zero padded)
+    __device__ uint64_t load8(uint32_t p) const {
+        const uint32_t w = p >> 2, sh = p & 3;
+        const uint32_t w0 = bw[w], w1 = bw[w + 1], w2 = bw[w + 2];
+        return (uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32 | __builtin_amdgcn_alignbyte(w1, w0, sh);
+    }
+    // common prefix of positions i and q (first words wi, wq already loaded), capped at nice
+    __device__ uint32_t lcp(uint32_t i, uint32_t q, uint32_t wi, uint32_t wq, uint32_t nice) const {
+        uint32_t x = wi ^ wq, cl;
+        if (x) {
+            cl = (uint32_t)__builtin_ctz(x) >> 3;
+        } else {
+            cl = 4;
+            while (cl < nice) {
+                const uint64_t y = load8(i + cl) ^ load8(q + cl);
+                if (y) {
+                    cl += (uint32_t)__builtin_ctzll(y) >> 3;
+                    break;
+                }
+                cl += 8;
+            }
+        }
+        return cl < nice ? cl : nice;
+    }
+    // Can candidate q beat a match of length thr (>= 4) at i?  Only if the 4 bytes ending
+    // at offset thr agree (wthr = load4(i + thr - 3)); zlib's scan_end test, widened.
+    __device__ bool may_beat(uint32_t q, uint32_t thr, uint32_t wthr) const {
+        return thr < 4 || load4(q + thr - 3) == wthr;
+    }
+
+    // ---- longest_match for every position at once (position-parallel) -----------------
+    // zlib's longest_match(i) depends on prev_length only through the chain limit (4096 or
+    // 1024 candidates) and the final "longer than prev_length" test, so the walk over the
+    // first kPreCand chain candidates (nearest first) can run for all positions in
+    // parallel before the serial parse.  M[i] = best | bestq << 9 | (walk cut short) << 31
+    // with best = max over those candidates of min(LCP, nice), bestq the nearest achieving
+    // it.  A cut-short walk is finished by search() if the parse visits i.
+    static constexpr uint32_t kPreCand = 16;
+    __device__ __noinline__ void match_all(uint32_t npos, uint32_t len) {
+        const int l = lane_id();
+        for (uint32_t i0 = 0; i0 < npos; i0 += 64) {
+            const uint32_t i = i0 + (uint32_t)l;
+            if (i < npos) {
+                const uint32_t wi = load4(i), hi = hash3(wi);
+                const uint32_t nice = (len - i) < 258 ? (len - i) : 258;
+                int k = (int)R[i] - 1;
+                uint32_t best = 0, bestq = 0, wb = 0, s = 0;
+                for (; s < kPreCand && k >= 0; s++, k--) {
+                    const uint32_t q = S[k];
+                    const uint32_t wq = load4(q);
+                    // position 0 is zlib's NIL and the lowest position of its hash run
+                    if (q == 0 || hash3(wq) != hi) break;
+                    if (!may_beat(q, best, wb)) continue;
+                    const uint32_t cl = lcp(i, q, wi, wq, nice);
+                    if (cl > best) {
+                        best = cl;
+                        bestq = q;
+                        if (best >= nice) break;
+                        wb = best >= 4 ? load4(i + best - 3) : 0u;
+                    }
+                }
+                const bool cut = s == kPreCand && best < nice;
+                M[i] = best | bestq << 9 | (cut ? 1u << 31 : 0u);
+            }
+        }
+        wave_sync();
+    }
+
     // ---- longest_match over the sorted chain -------------------------------------------
-    // Returns the match length (> b0) or 0; *q_out = nearest candidate achieving it.
-    __device__ uint32_t search(uint32_t i, uint32_t b0, uint32_t len, uint32_t *q_out) {
+    // Resumes a walk cut short by match_all: candidates kPreCand.. of position i, starting
+    // from that walk's best / bestq.  Returns the match length (> b0) or 0; *q_out = the
+    // nearest candidate achieving it.
+    __device__ uint32_t search(uint32_t i, uint32_t b0, uint32_t len, uint32_t best, uint32_t bestq,
+                               uint32_t *q_out) {
         const int l = lane_id();
         const uint32_t C = b0 >= 32 ? 1024u : 4096u;
         const uint32_t nice = (len - i) < 258 ? (len - i) : 258;
         const uint32_t wi = load4(i);
         const uint32_t hi = hash3(wi);
         const int r = (int)R[i];
-        uint32_t examined = 0, best = 0, bestq = 0;
-        for (int kb = r - 1;; kb -= 64) {
+        uint32_t examined = kPreCand;
+        for (int kb = r - 1 - (int)kPreCand;; kb -= 64) {
+            const uint32_t thr = best > b0 ? best : b0;
+            if (thr >= nice) break; // no candidate can be longer (lengths are capped at nice)
+            const uint32_t wthr = thr >= 4 ? load4(i + thr - 3) : 0u;
             const int k = kb - l;
             const uint32_t ord = examined + (uint32_t)l;
             uint32_t q = k >= 0 ? S[k] : 0u;
@@ -281,25 +356,7 @@ struct SmallWave {
             uint64_t m = ballot(valid);
             uint32_t npre = ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m);
             if (npre == 0) break;
-            uint32_t cl = 0;
-            if ((uint32_t)l < npre) {
-                uint32_t x = wi ^ wq;
-                if (x) {
-                    cl = (uint32_t)__builtin_ctz(x) >> 3;
-                } else {
-                    cl = 4;
-                    while (cl < nice) {
-                        x = load4(i + cl) ^ load4(q + cl);
-                        if (x) {
-                            cl += (uint32_t)__builtin_ctz(x) >> 3;
-                            break;
-                        }
-                        cl += 4;
-                    }
-                }
-                cl = cl < nice ? cl : nice;
-            }
-            const uint32_t thr = best > b0 ? best : b0;
+            const uint32_t cl = (uint32_t)l < npre && may_beat(q, thr, wthr) ? lcp(i, q, wi, wq, nice) : 0u;
             uint64_t mm = ballot(cl > thr);
             if (mm) {
                 int src;
@@ -633,7 +690,7 @@ struct SmallWave {
         for (int s = l; s < 352; s += 64) lfreq[s] = 0; // lfreq, dfreq, blfreq contiguous
         wave_sync();
         for (uint32_t t = l; t < ntok; t += 64) {
-            const uint32_t tk = tok[t], dist = tk >> 16, lc = tk & 0xff;
+            const uint32_t tk = tok[t], dist = tk >> 16, lc = dist ? tk & 0xff : b[tk & 0xffff];
             if (dist == 0) {
                 lds_add(&lfreq[lc], 1u);
             } else {
@@ -764,7 +821,7 @@ struct SmallWave {
             uint32_t nb = 0;
             uint64_t v = 0;
             if (t < ntok) {
-                const uint32_t tk = tok[t], dist = tk >> 16, lc = tk & 0xff;
+                const uint32_t tk = tok[t], dist = tk >> 16, lc = dist ? tk & 0xff : b[tk & 0xffff];
                 if (dist == 0) {
                     const uint32_t c = lcode[lc];
                     v = c & 0xffff;
@@ -833,12 +890,19 @@ struct SmallWave {
         const uint32_t crc = wave_crc32(b, len, crc_tab);
         stamp(0);
         const uint32_t npos = len >= 3 ? len - 2 : 0;
-        if (npos) sort_positions(npos);
+        if (npos) {
+            sort_positions(npos);
+            match_all(npos, len);
+        }
         stamp(1);
-        // deflate_slow over the sorted chains (single block: len < 16383 symbols)
+        // deflate_slow over the precomputed matches (single block: len < 16383 symbols).
+        // M[] is read 64 entries at a time into a VGPR window and indexed with readlane, so a
+        // step costs scalar work only.  Tokens: match = (dist << 16) | (len - 3); literal =
+        // its position (dist 0), the byte is fetched in flush.
         uint32_t i = 0, match_length = 2, prev_length, ntok = 0, treg = 0;
         uint32_t match_start = 0, prev_match;
         bool match_available = false;
+        uint32_t wbase = 0xffff0000u, wm = 0;
         auto emit = [&](uint32_t token) {
             if ((uint32_t)l == (ntok & 63)) treg = token;
             if ((ntok & 63) == 63) tok[ntok - 63 + l] = treg;
@@ -849,8 +913,14 @@ struct SmallWave {
             prev_match = match_start;
             match_length = 2;
             if (i + 3 <= len && prev_length < 258) {
-                uint32_t q = 0;
-                const uint32_t m = search(i, prev_length, len, &q);
+                if (i - wbase >= 64) {
+                    wbase = i;
+                    wm = i + (uint32_t)l < npos ? M[i + l] : 0u;
+                }
+                const uint32_t e = readlane(wm, (int)(i - wbase));
+                uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
+                if (e >> 31) m = search(i, prev_length, len, m, q, &q);
+                else if (m <= prev_length) m = 0;
                 if (m) {
                     match_length = m;
                     match_start = q;
@@ -863,14 +933,14 @@ struct SmallWave {
                 match_available = false;
                 match_length = 2;
             } else if (match_available) {
-                emit(b[i - 1]);
+                emit(i - 1);
                 i++;
             } else {
                 match_available = true;
                 i++;
             }
         }
-        if (match_available) emit(b[i - 1]);
+        if (match_available) emit(i - 1);
         if ((ntok & 63) != 0 && (uint32_t)l < (ntok & 63)) tok[(ntok & ~63u) + l] = treg;
         wave_sync_global();
         stamp(2);
@@ -937,6 +1007,7 @@ __global__ void __launch_bounds__(256) deflate_small_kernel(DeflateArgs a) {
     w.T = to_lds<uint16_t>(W + L.T);
     w.H = to_lds<uint16_t>(W + L.H);
     w.cnt = to_lds<uint16_t>(W + L.cnt);
+    w.M = to_lds<uint32_t>(W + L.T);
     w.tok = (PMC_GLB uint32_t *)(a.tokens + wave * kSlabSyms);
     w.fb = reinterpret_cast<Trees *>(a.scratch + wave * sizeof(Trees));
     w.crc_tab = to_lds<const uint32_t>(crc_tab);

@@ -208,6 +208,18 @@ struct InflateWave {
     uint8_t *inb; // staged input (LDS) or src (HBM variant)
     uint8_t *out; // output image (LDS) or dst (HBM variant)
     const uint32_t *crc_tab;
+    uint64_t st[8];
+    uint64_t t_last;
+
+    // PMC_STAMPS: 0 stage+header, 1 block headers + code lengths, 2 table builds,
+    // 3 symbol decode, 4 materialise, 5 trailer (CRC) + copy-out
+    __device__ void stamp(int k) {
+#ifdef PMC_STAMPS
+        uint64_t t = __builtin_amdgcn_s_memtime();
+        st[k] += t - t_last;
+        t_last = t;
+#endif
+    }
 
     __device__ void sync() {
         if (kHbm) wave_sync_global();
@@ -298,6 +310,7 @@ struct InflateWave {
         hrc = rfl(hrc);
         if (hrc) return hrc;
         p = rfl64(p);
+        stamp(0);
         Bits<!kHbm> br{inb, in_len * 8, p * 8};
         uint64_t outn = 0; // bytes produced (uniform)
         int last = 0;
@@ -346,8 +359,10 @@ struct InflateWave {
                 // fixed code lengths (inflate.c fixedtables)
                 for (int s = l; s < 320; s += 64) sc->lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
                 sync();
+                stamp(1);
                 huff_build(sc->lit, sc->lens, 288, false);
                 huff_build(sc->dist, sc->lens + 288, 32, false);
+                stamp(2);
             } else {
                 // dynamic: HLIT/HDIST/HCLEN, code-length code, then the code lengths
                 int nlen = 0, ndist = 0, ncode = 0;
@@ -374,7 +389,9 @@ struct InflateWave {
                 rc = rfl(rc);
                 if (rc) return rc;
                 sync();
+                stamp(1);
                 if (huff_build(sc->cl, sc->lens, 19, true)) return PMC_Z_DATA_ERROR_DEV;
+                stamp(2);
                 nlen = rfl(nlen);
                 ndist = rfl(ndist);
                 if (l == 0) {
@@ -422,8 +439,10 @@ struct InflateWave {
                 if (rc) return rc;
                 br.pos = rfl64(br.pos);
                 sync();
+                stamp(1);
                 if (huff_build(sc->lit, sc->lens, nlen, false)) return PMC_Z_DATA_ERROR_DEV;
                 if (huff_build(sc->dist, sc->lens + 288, ndist, false)) return PMC_Z_DATA_ERROR_DEV;
+                stamp(2);
             }
             // ---- symbol decode (lane 0) + materialisation (wave) ----
             for (;;) {
@@ -467,7 +486,9 @@ struct InflateWave {
                 rel = rfl(rel);
                 br.pos = rfl64(br.pos);
                 sync();
+                stamp(3);
                 materialise(nt, outn, cap);
+                stamp(4);
                 outn += rel;
                 if (st < 0) return st;
                 if (st == 1) break;
@@ -497,6 +518,7 @@ struct InflateWave {
             }
         }
         if (l == 0) *dst_len = (uint32_t)outn;
+        stamp(5);
         return 0;
     }
 };
@@ -517,6 +539,10 @@ __global__ void __launch_bounds__(256) inflate_kernel(InflateArgs a) {
     InflateWave<kHbm> W;
     W.sc = reinterpret_cast<InflateScratch *>(base + L.scr);
     W.crc_tab = crc_tab;
+    for (int k = 0; k < 8; k++) W.st[k] = 0;
+#ifdef PMC_STAMPS
+    W.t_last = __builtin_amdgcn_s_memtime();
+#endif
     // groups of 64 members per wave; this variant's members picked out by ballot
     for (uint64_t g = wave * 64; g < a.n; g += nwaves * 64) {
       const uint64_t vl = g + (uint64_t)l;
@@ -556,6 +582,10 @@ __global__ void __launch_bounds__(256) inflate_kernel(InflateArgs a) {
         }
       }
     }
+#ifdef PMC_STAMPS
+    if (l == 0 && a.dbg)
+        for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&a.dbg[k], (unsigned long long)W.st[k]);
+#endif
 }
 
 template __global__ void inflate_kernel<false>(InflateArgs);

@@ -51,6 +51,7 @@ struct InflateArgs {
     uint64_t lds_max_in;
     uint64_t wave_bytes;
     uint8_t *scratch;
+    uint64_t *dbg; // PMC_STAMPS builds: per-phase cycle sums (slots 0..7 deflate-independent)
 };
 
 uint64_t deflate_wave_bytes(bool hbm, uint64_t n);

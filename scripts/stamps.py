@@ -15,8 +15,11 @@ import torch  # noqa: E402
 import pmc_codec  # noqa: E402
 from pmc_codec import device as D  # noqa: E402
 
-PHASES = ["stage+crc", "hash+sort", "parse", "trees lit+dist (rest)", "emit", "trailer+copy", "zero+histogram",
-          "runs+bl tree (rest)", "bt:leaves", "bt:heap", "bt:depths", "bt:sums", "bt:codes", "-", "-", "-"]
+PHASES = ["stage+crc", "hash+sort+match_all", "parse", "trees lit+dist (rest)", "emit", "trailer+copy",
+          "zero+histogram", "runs+bl tree (rest)", "bt:leaves", "bt:heap", "bt:depths", "bt:sums", "bt:codes", "-",
+          "-", "-"]
+IPHASES = ["inf:stage+header", "inf:block hdr+code lens", "inf:table builds", "inf:symbol decode",
+           "inf:materialise", "inf:crc+copy", "-", "-"]
 
 
 def main():
@@ -25,7 +28,7 @@ def main():
     d = os.path.join(ROOT, "tests", "golden", "data")
     corpus_b = b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)))
     corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).cuda()
-    dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros(32, dtype=torch.int64, device="cuda")
     L.pmc_debug_stamps(ctx.handle, dbg.data_ptr())
     for vlen, kind, n in ((1024, 0, 400_000), (256, 0, 400_000), (4096, 0, 100_000), (1024, 1, 200_000)):
         data = torch.empty(n * vlen + 16, dtype=torch.uint8, device="cuda")
@@ -37,12 +40,16 @@ def main():
         torch.cuda.synchronize()
         out, rc = D.compress(ctx, D.Batch(data, off, lens, n, vlen))
         torch.cuda.synchronize()
+        back, brc = D.decompress(ctx, out, [vlen] * n)
+        torch.cuda.synchronize()
         s = dbg.cpu().tolist()
-        tot = sum(s)
-        print(f"vlen={vlen} kind={kind} n={n}: wave-cycles/value total {tot / n:,.0f}  rc!=0: {int((rc != 0).sum())}")
-        for k, name in enumerate(PHASES):
-            if s[k]:
-                print(f"   {name:16s} {s[k] / n:12,.0f}  {100 * s[k] / tot:5.1f}%")
+        for lo, names, what in ((0, PHASES, "deflate"), (16, IPHASES, "inflate")):
+            tot = sum(s[lo:lo + 16])
+            bad = int((rc != 0).sum()) if lo == 0 else int((brc != 0).sum())
+            print(f"vlen={vlen} kind={kind} n={n} {what}: wave-cycles/value total {tot / n:,.0f}  rc!=0: {bad}")
+            for k, name in enumerate(names):
+                if s[lo + k]:
+                    print(f"   {name:24s} {s[lo + k] / n:12,.0f}  {100 * s[lo + k] / tot:5.1f}%")
     ctx.close()
 
 

@@ -224,6 +224,50 @@ int main(int argc, char **argv) {
         }
         return best > b0 ? best : 0;
     };
+    // v2 small-value path (pmc_deflate_small.hip match_all + search): every position's walk
+    // over its first kPre chain candidates is done up front (best | q << 9 | cut << 31);
+    // the parse resumes cut walks at candidate kPre.
+    const uint32_t kPre = 16;
+    const bool pre = use_v2 && len <= 16382;
+    std::vector<uint32_t> M(pre ? npos : 0);
+    for (uint64_t i = 0; pre && i < npos; i++) {
+        uint32_t nice = (uint32_t)((len - i) < 258 ? (len - i) : 258), best = 0, bq = 0, s = 0;
+        int64_t k = (int64_t)rank[i] - 1;
+        for (; s < kPre && k >= 0; s++, k--) {
+            uint64_t q = S[k] & 0xffffffffull;
+            if (q == 0 || (S[k] >> 32) != (S[rank[i]] >> 32)) break;
+            uint32_t l = 0;
+            while (l < nice && b[i + l] == b[q + l]) l++;
+            if (l > best) {
+                best = l;
+                bq = (uint32_t)q;
+                if (best >= nice) break;
+            }
+        }
+        M[i] = best | bq << 9 | ((s == kPre && best < nice) ? 1u << 31 : 0u);
+    }
+    auto search_pre = [&](uint64_t i, uint32_t b0, uint64_t *qo) -> uint32_t {
+        uint32_t best = M[i] & 511;
+        *qo = (M[i] >> 9) & 0x3fff;
+        if (M[i] >> 31) {
+            uint32_t C = b0 >= 32 ? 1024 : 4096;
+            uint32_t nice = (uint32_t)((len - i) < 258 ? (len - i) : 258);
+            int64_t r = (int64_t)rank[i];
+            uint32_t ex = kPre;
+            for (int64_t k = r - 1 - kPre; k >= 0 && ex < C; k--, ex++) {
+                uint64_t q = S[k] & 0xffffffffull;
+                if ((S[k] >> 32) != (S[r] >> 32) || q == 0) break;
+                uint32_t l = 0;
+                while (l < nice && b[i + l] == b[q + l]) l++;
+                if (l > best) {
+                    best = l;
+                    *qo = q;
+                    if (l >= nice) break;
+                }
+            }
+        }
+        return best > b0 ? best : 0;
+    };
     std::vector<uint8_t> out(10, 0);
     const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 2, 3};
     memcpy(out.data(), hdr, 10);
@@ -354,7 +398,7 @@ int main(int argc, char **argv) {
         match_length = 2;
         if (i + 3 <= len && prev_length < 258) {
             uint64_t q = 0;
-            uint32_t m = search(i, prev_length, B, &q);
+            uint32_t m = pre ? search_pre(i, prev_length, &q) : search(i, prev_length, B, &q);
             if (m) {
                 match_length = m;
                 match_start = q;
