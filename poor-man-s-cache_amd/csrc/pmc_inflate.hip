@@ -70,9 +70,6 @@ __host__ __device__ inline InflateLayout inflate_layout(uint64_t max_out, uint64
     L.total = a16(off);
     return L;
 }
-uint64_t inflate_wave_bytes(bool hbm, uint64_t max_out, uint64_t max_in) {
-    return hbm ? inflate_layout<true>(max_out, max_in).total : inflate_layout<false>(max_out, max_in).total;
-}
 
 // Build count/offs/symbol (lane 0) and the fast table (wave).  Returns 0 or -1 (inftrees
 // over-subscribed / incomplete rule); is_codes selects the stricter code-length-code rule.
@@ -523,6 +520,519 @@ struct InflateWave {
     }
 };
 
+// =====================================================================================
+// LDS-resident members (the hot path).  Same verdicts and bit consumption order as the
+// general InflateWave above (oracle/inflate.c), organised for latency:
+//  * headers and code lengths: wave-uniform bit buffer in SGPRs; the code-length code's
+//    7-bit table lives in two VGPRs (v_readlane lookup, no LDS round trip per symbol);
+//  * code tables: built by the whole wave (per-length counts and in-length ranks by
+//    ballot, canonical codes by shuffle) -- no serial per-symbol loop;
+//  * literal/length + distance symbols: every lane decodes at one of the 64 bit offsets
+//    W + lane of a window (two LDS round trips per window), then a scalar chase walks the
+//    tokens through the window with v_readlane only;
+//  * tokens of a batch stay in VGPRs (lane t holds token t) until materialised.
+// =====================================================================================
+struct InfTables {
+    uint16_t lfast[1 << kRootBits]; // lit/len root table: sym | len << 9, kEntLong, kEntInvalid
+    uint16_t dfast[1 << kRootBits];
+    uint16_t lsym[288]; // canonical symbol order (read only for codes longer than the root)
+    uint16_t dsym[32];
+    uint16_t lens[320];
+};
+struct InfLdsLayout {
+    uint64_t tab, in, out, total;
+};
+__host__ __device__ inline InfLdsLayout inf_lds_layout(uint64_t max_out, uint64_t max_in) {
+    InfLdsLayout L;
+    uint64_t off = 0;
+    L.tab = off;
+    off += a16(sizeof(InfTables));
+    L.in = off;
+    off += a16(max_in + 64); // zero padding: windows read up to 3 dwords past the bit position
+    L.out = off;
+    off += a16(max_out + 16);
+    L.total = a16(off);
+    return L;
+}
+
+// wave-uniform LSB-first bit reader over the LDS-staged member
+struct SBits {
+    PMC_LDS const uint32_t *w;
+    uint64_t bb;
+    uint32_t bn, wi, nbits;
+    __device__ uint32_t pos() const { return wi * 32 - bn; }
+    __device__ void refill() {
+        if (bn <= 32) {
+            bb |= (uint64_t)rfl(w[wi]) << bn;
+            wi++;
+            bn += 32;
+        }
+    }
+    __device__ void seek(uint32_t p) {
+        wi = p >> 5;
+        bb = 0;
+        bn = 0;
+        refill();
+        bb >>= (p & 31);
+        bn -= (p & 31);
+        refill(); // >= 33 bits buffered
+    }
+    __device__ uint32_t peek(uint32_t n) const { return (uint32_t)bb & ((1u << n) - 1); }
+    __device__ void drop(uint32_t n) {
+        bb >>= n;
+        bn -= n;
+    }
+    __device__ bool need(uint32_t n) const { return pos() + n <= nbits; }
+};
+
+uint64_t inflate_wave_bytes(bool hbm, uint64_t max_out, uint64_t max_in) {
+    return hbm ? inflate_layout<true>(max_out, max_in).total : inf_lds_layout(max_out, max_in).total;
+}
+
+struct InflateLds {
+    PMC_LDS InfTables *T;
+    PMC_LDS uint8_t *inb;
+    PMC_LDS uint32_t *inw;
+    PMC_LDS uint8_t *out;
+    PMC_LDS const uint32_t *crc_tab;
+    uint32_t lenv, distv; // lane s: base | extra bits << 16 (length codes 257+s, distance codes s)
+    uint64_t st[8];
+    uint64_t t_last;
+
+    // PMC_STAMPS: 0 stage+header, 1 block headers + code lengths, 2 table builds,
+    // 3 symbol decode, 4 materialise, 5 trailer (CRC) + copy-out
+    __device__ void stamp(int k) {
+#ifdef PMC_STAMPS
+        uint64_t t = __builtin_amdgcn_s_memtime();
+        st[k] += t - t_last;
+        t_last = t;
+#endif
+    }
+
+    // inftrees.c rules + root table for lens[0..n) (NC chunks of 64 symbols).  Returns 0 or
+    // -1 (over-subscribed, or incomplete where not allowed).  cntv: lane L = count[L].
+    template <int NC>
+    __device__ int build(PMC_LDS const uint16_t *lens, int n, bool is_codes, PMC_LDS uint16_t *fast,
+                         PMC_LDS uint16_t *symtab, uint32_t &cntv, int &maxo) {
+        const int l = lane_id();
+        uint32_t cnt[16];
+#pragma unroll
+        for (int L = 0; L < 16; L++) cnt[L] = 0;
+        uint32_t lc[NC], rk[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const int s = c * 64 + l;
+            const uint32_t len = s < n ? lens[s] : 0u;
+            uint32_t r = 0;
+#pragma unroll
+            for (int L = 1; L <= 15; L++) {
+                const uint64_t m = ballot(len == (uint32_t)L);
+                if (len == (uint32_t)L) r = cnt[L] + popc_lt(m);
+                cnt[L] += (uint32_t)__builtin_popcountll(m);
+            }
+            lc[c] = len;
+            rk[c] = r;
+        }
+        int mx = 0;
+#pragma unroll
+        for (int L = 1; L <= 15; L++)
+            if (cnt[L]) mx = L;
+        maxo = mx;
+        cntv = 0;
+        if (mx == 0) { // no codes: every pattern is invalid (zlib's 1-bit invalid marker)
+            for (int e = l; e < (1 << kRootBits); e += 64) fast[e] = kEntInvalid;
+            wave_sync();
+            return 0;
+        }
+        int left = 1;
+        bool bad = false;
+        uint32_t fv = 0, ov = 0, code = 0, off = 0;
+#pragma unroll
+        for (int L = 1; L <= 15; L++) {
+            left <<= 1;
+            left -= (int)cnt[L];
+            bad |= left < 0;
+            fv = l == L ? code : fv; // canonical first code of length L
+            ov = l == L ? off : ov;  // index of its first symbol in symtab
+            cntv = l == L ? cnt[L] : cntv;
+            code = (code + cnt[L]) << 1;
+            off += cnt[L];
+        }
+        if (bad || (left > 0 && (is_codes || mx != 1))) return -1;
+        if (left > 0) { // incomplete (a single 1-bit code): the other half stays invalid
+            for (int e = l; e < (1 << kRootBits); e += 64) fast[e] = kEntInvalid;
+            wave_sync();
+        }
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const uint32_t len = lc[c];
+            const uint32_t f = (uint32_t)__shfl((int)fv, (int)len), o = (uint32_t)__shfl((int)ov, (int)len);
+            if (len) {
+                const uint32_t s = (uint32_t)(c * 64 + l);
+                const uint32_t rev = __builtin_bitreverse32(f + rk[c]) >> (32 - len);
+                if (len <= (uint32_t)kRootBits) {
+                    const uint16_t ent = (uint16_t)(s | len << 9);
+                    for (uint32_t e = rev; e < (1u << kRootBits); e += 1u << len) fast[e] = ent;
+                } else {
+                    fast[rev & ((1u << kRootBits) - 1)] = kEntLong;
+                }
+                if (mx > kRootBits) symtab[o + rk[c]] = (uint16_t)s;
+            }
+        }
+        wave_sync();
+        return 0;
+    }
+
+    // canonical decode of a code longer than the root (complete codes only: always found)
+    __device__ uint32_t slow_decode(uint32_t bits, uint32_t cntv, PMC_LDS const uint16_t *symtab,
+                                    uint32_t &L) {
+        int code = 0, first = 0, index = 0;
+        for (int len = 1; len <= 15; len++) {
+            code |= (int)((bits >> (len - 1)) & 1u);
+            const int count = (int)readlane(cntv, len);
+            if (code - count < first) {
+                L = (uint32_t)len;
+                return rfl((uint32_t)symtab[index + (code - first)]);
+            }
+            index += count;
+            first += count;
+            first <<= 1;
+            code <<= 1;
+        }
+        L = 15;
+        return 0xffffu;
+    }
+
+    // lanes: 32 stream bits at W + lane, and the root-table entries they index
+    __device__ void window(uint32_t W, uint32_t &bits, uint32_t &le, uint32_t &de) const {
+        const uint32_t p = W + (uint32_t)lane_id();
+        const uint32_t lo = inw[p >> 5], hi = inw[(p >> 5) + 1];
+        bits = __builtin_amdgcn_alignbit(hi, lo, p & 31);
+        le = T->lfast[bits & ((1u << kRootBits) - 1)];
+        de = T->dfast[bits & ((1u << kRootBits) - 1)];
+    }
+
+    // write the batch's tokens: literals in one store, then matches in stream order
+    __device__ void materialise(uint32_t nt, uint32_t tokv, uint32_t tposv, uint32_t o0, uint32_t cap) {
+        const uint32_t l = (uint32_t)lane_id();
+        const bool act = l < nt;
+        const uint32_t p = o0 + tposv;
+        if (act && !(tokv >> 31) && p < cap) out[p] = (uint8_t)tokv;
+        uint64_t mm = ballot(act && (tokv >> 31));
+        while (mm) {
+            const int j = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            const uint32_t t = readlane(tokv, j), pj = o0 + readlane(tposv, j);
+            const uint32_t len = (t & 0xff) + 3, dist = ((t >> 8) & 0x7fff) + 1, src0 = pj - dist;
+            if (dist >= len) {
+                for (uint32_t k = l; k < len; k += 64) {
+                    const uint32_t s = src0 + k;
+                    const uint8_t v = s < cap ? out[s] : (uint8_t)0;
+                    if (pj + k < cap) out[pj + k] = v;
+                }
+            } else { // overlapping copy: period dist
+                for (uint32_t k = l; k < len; k += 64) {
+                    const uint32_t s = src0 + k % dist;
+                    const uint8_t v = s < cap ? out[s] : (uint8_t)0;
+                    if (pj + k < cap) out[pj + k] = v;
+                }
+            }
+        }
+        wave_sync();
+    }
+
+    __device__ int run(const uint8_t *src, uint32_t in_len, uint8_t *dst, uint32_t cap, uint32_t *dst_len) {
+        const int l = lane_id();
+        // 1. stage input, zero padded by 64 bytes
+        {
+            const uint32_t words = (in_len + 64 + 3) >> 2;
+            if ((((uintptr_t)src) & 3) == 0) {
+                const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src);
+                const uint32_t full = in_len >> 2;
+                for (uint32_t k = l; k < words; k += 64) inw[k] = k < full ? s4[k] : 0u;
+                wave_sync();
+                if ((uint32_t)l < (in_len & 3)) inb[full * 4 + l] = src[full * 4 + l];
+            } else {
+                for (uint32_t k = l; k < words; k += 64) inw[k] = 0;
+                wave_sync();
+                for (uint32_t k = l; k < in_len; k += 64) inb[k] = src[k];
+            }
+            wave_sync();
+        }
+        // 2. gzip header (lane 0; inflate.c HEAD..HCRC)
+        int hrc = 0;
+        uint32_t p = 0;
+        if (l == 0) {
+            do {
+                if (in_len < 2) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                if (inb[0] != 0x1f || inb[1] != 0x8b) { hrc = PMC_Z_DATA_ERROR_DEV; break; }
+                if (in_len < 4) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                if (inb[2] != 8) { hrc = PMC_Z_DATA_ERROR_DEV; break; }
+                const uint32_t flg = inb[3];
+                if (flg & 0xe0) { hrc = PMC_Z_DATA_ERROR_DEV; break; }
+                if (in_len < 10) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                p = 10;
+                if (flg & 0x04) {
+                    if (in_len < p + 2) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                    const uint32_t xlen = inb[p] | ((uint32_t)inb[p + 1] << 8);
+                    p += 2;
+                    if (in_len < p + xlen) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                    p += xlen;
+                }
+                if (flg & 0x08) {
+                    while (p < in_len && inb[p] != 0) p++;
+                    if (p >= in_len) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                    p++;
+                }
+                if (flg & 0x10) {
+                    while (p < in_len && inb[p] != 0) p++;
+                    if (p >= in_len) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                    p++;
+                }
+                if (flg & 0x02) {
+                    if (in_len < p + 2) { hrc = PMC_Z_BUF_ERROR_DEV; break; }
+                    uint32_t hc = inb[p] | ((uint32_t)inb[p + 1] << 8), c = 0xFFFFFFFFu;
+                    for (uint32_t k = 0; k < p; k++) c = crc_tab[(c ^ inb[k]) & 0xff] ^ (c >> 8);
+                    if (hc != ((~c) & 0xffff)) { hrc = PMC_Z_DATA_ERROR_DEV; break; }
+                    p += 2;
+                }
+            } while (0);
+        }
+        hrc = rfl(hrc);
+        if (hrc) return hrc;
+        p = rfl(p);
+        stamp(0);
+        const uint32_t nbits = in_len * 8;
+        SBits sb{inw, 0, 0, 0, nbits};
+        sb.seek(p * 8);
+        uint32_t o = 0; // bytes produced (uniform)
+        uint32_t last;
+        do {
+            sb.refill();
+            if (!sb.need(3)) return PMC_Z_BUF_ERROR_DEV;
+            last = sb.peek(1);
+            const uint32_t type = (sb.peek(3) >> 1) & 3;
+            sb.drop(3);
+            if (type == 0) { // stored
+                sb.seek((sb.pos() + 7) & ~7u);
+                if (!sb.need(32)) return PMC_Z_BUF_ERROR_DEV;
+                const uint32_t len = sb.peek(16);
+                sb.drop(16);
+                const uint32_t nlen = sb.peek(16);
+                sb.drop(16);
+                if (len != (nlen ^ 0xffff)) return PMC_Z_DATA_ERROR_DEV;
+                if (!sb.need(8 * len)) return PMC_Z_BUF_ERROR_DEV;
+                const uint32_t ib = sb.pos() >> 3;
+                for (uint32_t k = l; k < len; k += 64)
+                    if (o + k < cap) out[o + k] = inb[ib + k];
+                o += len;
+                sb.seek(sb.pos() + 8 * len);
+                wave_sync();
+                continue;
+            }
+            if (type == 3) return PMC_Z_DATA_ERROR_DEV;
+            uint32_t lcnt = 0, dcnt = 0;
+            int lmax = 0, dmax = 0;
+            if (type == 1) { // fixed code lengths (inflate.c fixedtables)
+                for (int s = l; s < 320; s += 64)
+                    T->lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+                wave_sync();
+                stamp(1);
+                build<5>(T->lens, 288, false, T->lfast, T->lsym, lcnt, lmax);
+                build<1>(T->lens + 288, 32, false, T->dfast, T->dsym, dcnt, dmax);
+                stamp(2);
+            } else { // dynamic
+                sb.refill();
+                if (!sb.need(14)) return PMC_Z_BUF_ERROR_DEV;
+                const uint32_t nlen = sb.peek(5) + 257;
+                sb.drop(5);
+                const uint32_t ndist = sb.peek(5) + 1;
+                sb.drop(5);
+                const uint32_t ncode = sb.peek(4) + 4;
+                sb.drop(4);
+                if (nlen > 286 || ndist > 30) return PMC_Z_DATA_ERROR_DEV;
+                // code-length code lengths: lane k reads its 3 bits directly
+                const uint32_t p0 = sb.pos();
+                if (p0 + 3 * ncode > nbits) return PMC_Z_BUF_ERROR_DEV;
+                if (l < 19) {
+                    const uint32_t q = p0 + 3 * (uint32_t)l;
+                    const uint32_t v = __builtin_amdgcn_alignbit(inw[(q >> 5) + 1], inw[q >> 5], q & 31) & 7u;
+                    T->lens[c_cl_order[l]] = (uint16_t)((uint32_t)l < ncode ? v : 0u);
+                }
+                sb.seek(p0 + 3 * ncode);
+                wave_sync();
+                stamp(1);
+                uint32_t ccnt;
+                int clmax;
+                if (build<1>(T->lens, 19, true, T->lfast, T->lsym, ccnt, clmax)) return PMC_Z_DATA_ERROR_DEV;
+                stamp(2);
+                // the code-length code (<= 7 bits) as a 128-entry table in two VGPRs
+                const uint32_t cl0 = T->lfast[l], cl1 = T->lfast[64 + l];
+                const uint32_t total = nlen + ndist;
+                uint32_t have = 0, prev = 0;
+                while (have < total) {
+                    sb.refill();
+                    uint32_t sym;
+                    if (clmax == 0) { // zlib decodes 0 from its 1-bit invalid marker
+                        if (!sb.need(1)) return PMC_Z_BUF_ERROR_DEV;
+                        sb.drop(1);
+                        sym = 0;
+                    } else {
+                        const uint32_t idx = sb.peek(7);
+                        const uint32_t e = idx < 64 ? readlane(cl0, (int)idx) : readlane(cl1, (int)(idx - 64));
+                        const uint32_t L = e >> 9;
+                        if (!sb.need(L)) return PMC_Z_BUF_ERROR_DEV;
+                        sb.drop(L);
+                        sym = e & 0x1ff;
+                    }
+                    if (sym < 16) {
+                        T->lens[have] = (uint16_t)sym;
+                        prev = sym;
+                        have++;
+                    } else {
+                        uint32_t val = 0, copy;
+                        if (sym == 16) {
+                            if (!sb.need(2)) return PMC_Z_BUF_ERROR_DEV;
+                            if (have == 0) return PMC_Z_DATA_ERROR_DEV;
+                            val = prev;
+                            copy = 3 + sb.peek(2);
+                            sb.drop(2);
+                        } else if (sym == 17) {
+                            if (!sb.need(3)) return PMC_Z_BUF_ERROR_DEV;
+                            copy = 3 + sb.peek(3);
+                            sb.drop(3);
+                        } else {
+                            if (!sb.need(7)) return PMC_Z_BUF_ERROR_DEV;
+                            copy = 11 + sb.peek(7);
+                            sb.drop(7);
+                        }
+                        if (have + copy > total) return PMC_Z_DATA_ERROR_DEV;
+                        for (uint32_t k = l; k < copy; k += 64) T->lens[have + k] = (uint16_t)val;
+                        have += copy;
+                        prev = val;
+                    }
+                }
+                wave_sync();
+                if (rfl((uint32_t)T->lens[256]) == 0) return PMC_Z_DATA_ERROR_DEV;
+                stamp(1);
+                if (build<5>(T->lens, (int)nlen, false, T->lfast, T->lsym, lcnt, lmax)) return PMC_Z_DATA_ERROR_DEV;
+                if (build<1>(T->lens + nlen, (int)ndist, false, T->dfast, T->dsym, dcnt, dmax))
+                    return PMC_Z_DATA_ERROR_DEV;
+                stamp(2);
+            }
+            // ---- symbols: windowed speculative decode, batches of <= 64 tokens ----
+            uint32_t W = sb.pos(), x = 0, bits, le, de;
+            window(W, bits, le, de);
+            uint32_t pend = 0; // pending match length (its distance not decoded yet)
+            for (;;) {
+                uint32_t nt = 0, tokv = 0, tposv = 0;
+                const uint32_t o0 = o;
+                int stt = 0;
+                while (nt < 64) {
+                    if (x >= 64) {
+                        W += x;
+                        x = 0;
+                        window(W, bits, le, de);
+                    }
+                    const uint32_t pos = W + x;
+                    if (pend == 0) {
+                        const uint32_t e = readlane(le, (int)x);
+                        uint32_t L, sym;
+                        if (e < kEntInvalid) {
+                            L = e >> 9;
+                            sym = e & 0x1ff;
+                        } else if (e == kEntInvalid) {
+                            stt = pos + 1 > nbits ? PMC_Z_BUF_ERROR_DEV : PMC_Z_DATA_ERROR_DEV;
+                            break;
+                        } else {
+                            sym = slow_decode(readlane(bits, (int)x), lcnt, T->lsym, L);
+                        }
+                        if (pos + L > nbits) { stt = PMC_Z_BUF_ERROR_DEV; break; }
+                        if (sym < 256) {
+                            if ((uint32_t)l == nt) {
+                                tokv = sym;
+                                tposv = o - o0;
+                            }
+                            nt++;
+                            o++;
+                            x += L;
+                            continue;
+                        }
+                        if (sym == 256) {
+                            x += L;
+                            stt = 1;
+                            break;
+                        }
+                        const uint32_t s = sym - 257;
+                        if (s >= 29) { stt = PMC_Z_DATA_ERROR_DEV; break; }
+                        const uint32_t lv = readlane(lenv, (int)s), eb = lv >> 16;
+                        if (pos + L + eb > nbits) { stt = PMC_Z_BUF_ERROR_DEV; break; }
+                        pend = (lv & 0xffff) + ((readlane(bits, (int)x) >> L) & ((1u << eb) - 1));
+                        x += L + eb;
+                    } else {
+                        const uint32_t e = readlane(de, (int)x);
+                        uint32_t L, ds;
+                        if (e < kEntInvalid) {
+                            L = e >> 9;
+                            ds = e & 0x1ff;
+                        } else if (e == kEntInvalid) {
+                            stt = pos + 1 > nbits ? PMC_Z_BUF_ERROR_DEV : PMC_Z_DATA_ERROR_DEV;
+                            break;
+                        } else {
+                            ds = slow_decode(readlane(bits, (int)x), dcnt, T->dsym, L);
+                        }
+                        if (pos + L > nbits) { stt = PMC_Z_BUF_ERROR_DEV; break; }
+                        if (ds >= 30) { stt = PMC_Z_DATA_ERROR_DEV; break; }
+                        const uint32_t dv = readlane(distv, (int)ds), eb = dv >> 16;
+                        if (pos + L + eb > nbits) { stt = PMC_Z_BUF_ERROR_DEV; break; }
+                        const uint32_t dist = (dv & 0xffff) + ((readlane(bits, (int)x) >> L) & ((1u << eb) - 1));
+                        if (dist > o) { stt = PMC_Z_DATA_ERROR_DEV; break; }
+                        if ((uint32_t)l == nt) {
+                            tokv = 0x80000000u | (dist - 1) << 8 | (pend - 3);
+                            tposv = o - o0;
+                        }
+                        nt++;
+                        o += pend;
+                        pend = 0;
+                        x += L + eb;
+                    }
+                }
+                stamp(3);
+                materialise(nt, tokv, tposv, o0, cap);
+                stamp(4);
+                if (stt < 0) return stt;
+                if (stt == 1) break;
+            }
+            sb.seek(W + x);
+        } while (!last);
+        // 3. trailer: CRC-32 then ISIZE (inflate.c CHECK / LENGTH)
+        const uint32_t tp = (sb.pos() + 7) >> 3;
+        if (in_len < tp + 4) return PMC_Z_BUF_ERROR_DEV;
+        if (o > cap) return PMC_Z_DATA_ERROR_DEV;
+        const uint32_t crc = wave_crc32(out, o, crc_tab);
+        const uint32_t want = inb[tp] | ((uint32_t)inb[tp + 1] << 8) | ((uint32_t)inb[tp + 2] << 16) |
+                              ((uint32_t)inb[tp + 3] << 24);
+        if (crc != want) return PMC_Z_DATA_ERROR_DEV;
+        if (in_len < tp + 8) return PMC_Z_BUF_ERROR_DEV;
+        const uint32_t isz = inb[tp + 4] | ((uint32_t)inb[tp + 5] << 8) | ((uint32_t)inb[tp + 6] << 16) |
+                             ((uint32_t)inb[tp + 7] << 24);
+        if (isz != o) return PMC_Z_DATA_ERROR_DEV;
+        // 4. copy-out
+        if ((((uintptr_t)dst) & 3) == 0) {
+            uint32_t *d4 = reinterpret_cast<uint32_t *>(dst);
+            PMC_LDS const uint32_t *o4 = (PMC_LDS const uint32_t *)out;
+            const uint32_t full = o >> 2;
+            for (uint32_t k = l; k < full; k += 64) d4[k] = o4[k];
+            if ((uint32_t)l < (o & 3)) dst[full * 4 + l] = out[full * 4 + l];
+        } else {
+            for (uint32_t k = l; k < o; k += 64) dst[k] = out[k];
+        }
+        if (l == 0) *dst_len = o;
+        stamp(5);
+        return 0;
+    }
+};
+
 template <bool kHbm>
 __global__ void __launch_bounds__(256) inflate_kernel(InflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -535,56 +1045,70 @@ __global__ void __launch_bounds__(256) inflate_kernel(InflateArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * waves_per_block;
     const int l = lane_id();
     uint8_t *base = lds + 1024 + (uint64_t)wib * a.wave_bytes;
-    const InflateLayout L = inflate_layout<kHbm>(a.lds_max_out, a.lds_max_in);
-    InflateWave<kHbm> W;
-    W.sc = reinterpret_cast<InflateScratch *>(base + L.scr);
-    W.crc_tab = crc_tab;
-    for (int k = 0; k < 8; k++) W.st[k] = 0;
+    InflateWave<true> Wh;
+    InflateLds Wl;
+    if (kHbm) {
+        const InflateLayout L = inflate_layout<true>(a.lds_max_out, a.lds_max_in);
+        Wh.sc = reinterpret_cast<InflateScratch *>(base + L.scr);
+        Wh.crc_tab = crc_tab;
+        for (int k = 0; k < 8; k++) Wh.st[k] = 0;
+    } else {
+        const InfLdsLayout L = inf_lds_layout(a.lds_max_out, a.lds_max_in);
+        Wl.T = (PMC_LDS InfTables *)(base + L.tab);
+        Wl.inb = to_lds<uint8_t>(base + L.in);
+        Wl.inw = to_lds<uint32_t>(base + L.in);
+        Wl.out = to_lds<uint8_t>(base + L.out);
+        Wl.crc_tab = to_lds<const uint32_t>(crc_tab);
+        Wl.lenv = l < 29 ? (uint32_t)c_lbase[l] | (uint32_t)c_lext[l] << 16 : 0u;
+        Wl.distv = l < 30 ? (uint32_t)c_dbase[l] | (uint32_t)c_dext[l] << 16 : 0u;
+        for (int k = 0; k < 8; k++) Wl.st[k] = 0;
+    }
 #ifdef PMC_STAMPS
-    W.t_last = __builtin_amdgcn_s_memtime();
+    Wh.t_last = Wl.t_last = __builtin_amdgcn_s_memtime();
 #endif
     // groups of 64 members per wave; this variant's members picked out by ballot
     for (uint64_t g = wave * 64; g < a.n; g += nwaves * 64) {
-      const uint64_t vl = g + (uint64_t)l;
-      uint32_t my_in = 0, my_cap = 0;
-      if (vl < a.n) {
-          my_in = a.src_len[vl];
-          my_cap = a.dst_cap[vl];
-      }
-      const bool my_fits = my_cap <= a.lds_max_out && my_in <= a.lds_max_in;
-      uint64_t todo = ballot(vl < a.n && (kHbm != my_fits));
-      while (todo) {
-        const int j = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        const uint64_t v = g + (uint64_t)j;
-        const uint64_t in_len = rfl((uint32_t)__shfl(my_in, j));
-        const uint64_t cap = rfl((uint32_t)__shfl(my_cap, j));
-        const uint8_t *src = a.src + a.src_off[v];
-        uint8_t *dst = a.dst + a.dst_off[v];
-        if (in_len == 0) {
-            if (l == 0) {
-                a.rc[v] = PMC_INVALID_INPUT_DEV;
-                a.dst_len[v] = 0;
+        const uint64_t vl = g + (uint64_t)l;
+        uint32_t my_in = 0, my_cap = 0;
+        if (vl < a.n) {
+            my_in = a.src_len[vl];
+            my_cap = a.dst_cap[vl];
+        }
+        const bool my_fits = my_cap <= a.lds_max_out && my_in <= a.lds_max_in;
+        uint64_t todo = ballot(vl < a.n && (kHbm != my_fits));
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint64_t v = g + (uint64_t)j;
+            const uint32_t in_len = readlane(my_in, j);
+            const uint32_t cap = readlane(my_cap, j);
+            const uint8_t *src = a.src + a.src_off[v];
+            uint8_t *dst = a.dst + a.dst_off[v];
+            if (in_len == 0) {
+                if (l == 0) {
+                    a.rc[v] = PMC_INVALID_INPUT_DEV;
+                    a.dst_len[v] = 0;
+                }
+                continue;
             }
-            continue;
+            int rc;
+            if (kHbm) {
+                Wh.inb = const_cast<uint8_t *>(src);
+                Wh.out = dst;
+                rc = Wh.run(src, in_len, dst, cap, a.dst_len + v);
+            } else {
+                rc = Wl.run(src, in_len, dst, cap, a.dst_len + v);
+            }
+            if (l == 0) {
+                a.rc[v] = rc;
+                if (rc) a.dst_len[v] = 0;
+            }
         }
-        if (kHbm) {
-            W.inb = const_cast<uint8_t *>(src);
-            W.out = dst;
-        } else {
-            W.inb = base + L.in;
-            W.out = base + L.out;
-        }
-        int rc = W.run(src, in_len, dst, cap, a.dst_len + v);
-        if (l == 0) {
-            a.rc[v] = rc;
-            if (rc) a.dst_len[v] = 0;
-        }
-      }
     }
 #ifdef PMC_STAMPS
     if (l == 0 && a.dbg)
-        for (int k = 0; k < 8; k++) atomicAdd((unsigned long long *)&a.dbg[k], (unsigned long long)W.st[k]);
+        for (int k = 0; k < 8; k++)
+            atomicAdd((unsigned long long *)&a.dbg[k], (unsigned long long)(kHbm ? Wh.st[k] : Wl.st[k]));
 #endif
 }
 
