@@ -30,13 +30,16 @@ namespace pmc {
 
 constexpr uint32_t kSmallMax = 16382;
 
+// Per-wave LDS image (offsets from the wave's base).  Phases reuse dead regions:
+//   sort : bytes | S | R (hash keys until the ranks are written) | T, cnt
+//   parse: bytes | S | R | M (per-position match_all results)
+//   flush: bytes | out image, code tables, tree scratch, histograms (over S, R, M)
 struct SmallLayout {
-    uint64_t bytes, S, R, freq, W, total;
-    // inside W (flush phase)
-    uint64_t out, lcode, dcode, blcode, dad, dep, runs;
+    uint64_t bytes, S, R, X, total;
+    uint64_t out, lcode, dcode, blcode, dad, dep, runs, freq; // flush view
     uint64_t out_words;
-    // inside W (sort phase)
-    uint64_t T, H, cnt;
+    uint64_t T, cnt; // sort view
+    uint64_t M;      // parse view
 };
 
 __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
@@ -49,11 +52,9 @@ __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
     o += a(2 * n + 2);
     L.R = o;
     o += a(2 * n + 2);
-    L.freq = o; // lfreq u32[288], dfreq u32[32], blfreq u32[32]
-    o += 352 * 4;
-    L.W = o;
-    // flush view
-    uint64_t f = 0;
+    L.X = o;
+    // flush view, from S on
+    uint64_t f = L.S;
     L.out = f;
     L.out_words = a(gzip_bound(n) + 16) / 4;
     f += L.out_words * 4;
@@ -69,16 +70,20 @@ __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
     f += 576;
     L.runs = f; // run lengths at run starts: lit/len [0,288), dist [288,320)
     f += 320 * 2;
+    L.freq = f; // lfreq u32[288], dfreq u32[32], blfreq u32[32]
+    f += 352 * 4;
     // sort view
-    uint64_t s = 0;
+    uint64_t s = L.X;
     L.T = s;
-    s += a(2 * n + 2);
-    L.H = s;
     s += a(2 * n + 2);
     L.cnt = s;
     s += 16 * 64 * 2;
-    o += a(f > s ? f : s);
-    L.total = a(o);
+    // parse view
+    L.M = L.X;
+    const uint64_t m = L.X + a(4 * n);
+    uint64_t t = f > s ? f : s;
+    t = t > m ? t : m;
+    L.total = a(t);
     return L;
 }
 uint64_t deflate_small_wave_bytes(uint64_t n) { return small_layout(n).total; }
@@ -976,7 +981,7 @@ struct SmallWave {
     }
 };
 
-__global__ void __launch_bounds__(256) deflate_small_kernel(DeflateArgs a) {
+__global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
     for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
@@ -986,7 +991,6 @@ __global__ void __launch_bounds__(256) deflate_small_kernel(DeflateArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     uint8_t *base = lds + 1024 + (uint64_t)wib * a.wave_bytes;
     const SmallLayout L = small_layout(a.cap_len);
-    uint8_t *W = base + L.W;
     SmallWave w;
     w.b = to_lds<uint8_t>(base + L.bytes);
     w.bw = to_lds<uint32_t>(base + L.bytes);
@@ -995,19 +999,19 @@ __global__ void __launch_bounds__(256) deflate_small_kernel(DeflateArgs a) {
     w.lfreq = to_lds<uint32_t>(base + L.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;
-    w.outw = to_lds<uint32_t>(W + L.out);
-    w.outb = to_lds<uint8_t>(W + L.out);
+    w.outw = to_lds<uint32_t>(base + L.out);
+    w.outb = to_lds<uint8_t>(base + L.out);
     w.out_words = (uint32_t)L.out_words;
-    w.lcode = to_lds<uint32_t>(W + L.lcode);
-    w.dcode = to_lds<uint32_t>(W + L.dcode);
-    w.blcode = to_lds<uint32_t>(W + L.blcode);
-    w.dad = to_lds<uint16_t>(W + L.dad);
-    w.dep = to_lds<uint8_t>(W + L.dep);
-    w.runs = to_lds<uint16_t>(W + L.runs);
-    w.T = to_lds<uint16_t>(W + L.T);
-    w.H = to_lds<uint16_t>(W + L.H);
-    w.cnt = to_lds<uint16_t>(W + L.cnt);
-    w.M = to_lds<uint32_t>(W + L.T);
+    w.lcode = to_lds<uint32_t>(base + L.lcode);
+    w.dcode = to_lds<uint32_t>(base + L.dcode);
+    w.blcode = to_lds<uint32_t>(base + L.blcode);
+    w.dad = to_lds<uint16_t>(base + L.dad);
+    w.dep = to_lds<uint8_t>(base + L.dep);
+    w.runs = to_lds<uint16_t>(base + L.runs);
+    w.T = to_lds<uint16_t>(base + L.T);
+    w.H = w.R; // hash keys live in R until the ranks overwrite them
+    w.cnt = to_lds<uint16_t>(base + L.cnt);
+    w.M = to_lds<uint32_t>(base + L.M);
     w.tok = (PMC_GLB uint32_t *)(a.tokens + wave * kSlabSyms);
     w.fb = reinterpret_cast<Trees *>(a.scratch + wave * sizeof(Trees));
     w.crc_tab = to_lds<const uint32_t>(crc_tab);
