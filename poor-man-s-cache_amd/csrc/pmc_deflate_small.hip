@@ -129,45 +129,63 @@ struct RegHeap {
     }
 };
 
-// Small heaps (the common case): one VGPR holds entries 0..63 (entry k in lane k); two
-// VGPRs hold entries 0..127 interleaved (entry k in lane k>>1 of h[k&1]) so the two
-// children 2k, 2k+1 of node k sit in lane k of h0 and h1 -- one readlane each, no select.
-template <int NR>
-struct RegHeapN {
+// Small heaps (the common case), written so every level of pqdownheap is straight-line
+// scalar code (two v_readlane, a select, one masked v_cndmask) with no dynamic register
+// indexing.  RegHeap1: entries 1..63, entry k in lane k.  RegHeap2: entries 1..127
+// interleaved, entry k in lane k>>1 of (k odd ? h1 : h0), so the children 2k, 2k+1 of node
+// k sit in lane k of h0 and h1.
+// (a <= b) ? t : f on the scalar unit (uniform operands), kept out of lane-mask form
+__device__ __forceinline__ uint32_t s_sel_le(uint32_t a, uint32_t b, uint32_t t, uint32_t f) {
+    uint32_t r;
+    asm("s_cmp_le_u32 %1, %2\n\ts_cselect_b32 %0, %3, %4" : "=s"(r) : "s"(a), "s"(b), "s"(t), "s"(f) : "scc");
+    return r;
+}
+// Both small heaps keep every slot past heap_len (and slot 0) at ~0: a missing right child
+// then never wins the smaller() test, so no j < heap_len check is needed.
+struct RegHeap1 {
+    uint32_t h;
+    __device__ uint32_t get(int k) const { return readlane(h, k); }
+    __device__ void set(int k, uint32_t v) { h = writelane(h, v, k); }
+    __device__ void down(int k, int n) {
+        const uint32_t v = readlane(h, k), kv = v >> 10;
+        int j = k << 1;
+        while (j <= n) {
+            const uint32_t x0 = readlane(h, j), y = readlane(h, (j + 1) & 63);
+            const uint32_t kx = x0 >> 10, ky = y >> 10;
+            const uint32_t x = s_sel_le(ky, kx, y, x0);
+            const int jn = (int)s_sel_le(ky, kx, (uint32_t)j + 1, (uint32_t)j);
+            if (kv <= (x >> 10)) break;
+            h = writelane(h, x, k);
+            k = jn;
+            j = k << 1;
+        }
+        h = writelane(h, v, k);
+    }
+};
+struct RegHeap2 {
     uint32_t h0, h1;
     __device__ uint32_t get(int k) const {
-        if (NR == 1) return readlane(h0, k & 63);
-        return readlane((k & 1) ? h1 : h0, (k >> 1) & 63);
+        const uint32_t a = readlane(h0, k >> 1), b = readlane(h1, k >> 1);
+        return (k & 1) ? b : a;
     }
     __device__ void set(int k, uint32_t v) {
-        if (NR == 1) {
-            h0 = writelane(h0, v, k);
-        } else if (k & 1) {
-            h1 = writelane(h1, v, k >> 1);
-        } else {
-            h0 = writelane(h0, v, k >> 1);
-        }
+        const bool hit = lane_id() == (k >> 1);
+        const bool odd = (k & 1) != 0;
+        h0 = (hit & !odd) ? v : h0;
+        h1 = (hit & odd) ? v : h1;
     }
-    __device__ void down(int k, int heap_len) {
-        uint32_t v = get(k);
+    __device__ void down(int k, int n) {
+        const uint32_t v = get(k), kv = v >> 10;
         int j = k << 1;
-        while (j <= heap_len) {
-            uint32_t x, y;
-            if (NR == 1) {
-                x = readlane(h0, j & 63);
-                y = readlane(h0, (j + 1) & 63);
-            } else {
-                x = readlane(h0, k & 63);
-                y = readlane(h1, k & 63);
-            }
-            if (j < heap_len && (y >> 10) <= (x >> 10)) {
-                j++;
-                x = y;
-            }
-            if ((v >> 10) <= (x >> 10)) break;
+        while (j <= n) {
+            const uint32_t x0 = readlane(h0, k), y = readlane(h1, k);
+            const uint32_t kx = x0 >> 10, ky = y >> 10;
+            const uint32_t x = s_sel_le(ky, kx, y, x0);
+            const int jn = (int)s_sel_le(ky, kx, (uint32_t)j + 1, (uint32_t)j);
+            if (kv <= (x >> 10)) break;
             set(k, x);
-            k = j;
-            j <<= 1;
+            k = jn;
+            j = k << 1;
         }
         set(k, v);
     }
@@ -392,6 +410,7 @@ struct SmallWave {
         do {
             const uint32_t n = hp.get(1);
             hp.set(1, hp.get(heap_len));
+            hp.set(heap_len, ~0u);
             heap_len--;
             hp.down(1, heap_len);
             const uint32_t m = hp.get(1);
@@ -400,10 +419,8 @@ struct SmallWave {
             const uint32_t d = (dn >= dm ? dn : dm) + 1;
             deep |= d >= 31;
             const uint32_t key = (((kn >> 5) + (km >> 5)) << 5) | (d & 31);
-            if (l == 0) {
-                dad[n & 1023] = (uint16_t)node;
-                dad[m & 1023] = (uint16_t)node;
-            }
+            dad[n & 1023] = (uint16_t)node; // (all lanes store the same value: no exec change)
+            dad[m & 1023] = (uint16_t)node;
             hp.set(1, (key << 10) | (uint32_t)node);
             node++;
             hp.down(1, heap_len);
@@ -465,14 +482,13 @@ struct SmallWave {
         int node;
         bool deep = false;
         if (heap_len < 64) {
-            RegHeapN<1> hp;
-            hp.h0 = code_out[l];
-            hp.h1 = 0;
+            RegHeap1 hp;
+            hp.h = l >= 1 && l <= heap_len ? code_out[l] : ~0u;
             node = heap_merge(hp, heap_len, elems, deep);
         } else if (heap_len < 128) {
-            RegHeapN<2> hp;
-            hp.h0 = code_out[2 * l];
-            hp.h1 = code_out[2 * l + 1];
+            RegHeap2 hp;
+            hp.h0 = 2 * l >= 1 && 2 * l <= heap_len ? code_out[2 * l] : ~0u;
+            hp.h1 = 2 * l + 1 <= heap_len ? code_out[2 * l + 1] : ~0u;
             node = heap_merge(hp, heap_len, elems, deep);
         } else {
             RegHeap hp;
