@@ -282,7 +282,8 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
     if (n == 0) return PMC_OK;
     hipStream_t st = (hipStream_t)stream;
     DeflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, nullptr,
-                  ctx->dbg};
+                  ctx->dbg, -1};
+    if (const char *e = getenv("PMC_STOP_AFTER")) a.stop_after = atoi(e); // diagnostic builds only
     // Values <= small_lim: single-block LDS kernel (pmc_deflate_small.hip).  Larger values:
     // the general kernel with its working set in HBM (pmc_deflate.hip).  PMC_DEFLATE_V1=1
     // routes everything through the general kernels (A/B and safety net).

@@ -219,6 +219,7 @@ struct SmallWave {
     PMC_LDS const uint32_t *crc_tab;
     uint64_t st[16];
     uint64_t t_last;
+    int stop; // PMC_STAMPS: end the value after phase `stop` (instruction-count attribution)
 
     __device__ void stamp(int k) {
 #ifdef PMC_STAMPS
@@ -227,6 +228,12 @@ struct SmallWave {
         t_last = t;
 #endif
     }
+#ifdef PMC_STAMPS
+#define PMC_STOP(k, ret)                                                                                               \
+    if (stop == (k)) return ret;
+#else
+#define PMC_STOP(k, ret)
+#endif
 
     __device__ uint32_t load4(uint32_t p) const {
         uint32_t w0 = bw[p >> 2], w1 = bw[(p >> 2) + 1];
@@ -322,32 +329,66 @@ struct SmallWave {
     // with best = max over those candidates of min(LCP, nice), bestq the nearest achieving
     // it.  A cut-short walk is finished by search() if the parse visits i.
     static constexpr uint32_t kPreCand = 16;
+    // Work-stealing walk, branch-light: every iteration each lane issues the same loads
+    // (one chain entry, 8 bytes at i+off and at c+off, the two prune words) and advances
+    // its state with selects -- a candidate is fetched, pruned, or compared 8 bytes further.
+    // Lanes whose position is finished store M[i] and claim the next unclaimed position
+    // (ballot + popcount), so the iteration count follows the total work.  The only
+    // divergent blocks are that store/claim; per-lane control otherwise costs no SALU.
     __device__ __noinline__ void match_all(uint32_t npos, uint32_t len) {
-        const int l = lane_id();
-        for (uint32_t i0 = 0; i0 < npos; i0 += 64) {
-            const uint32_t i = i0 + (uint32_t)l;
-            if (i < npos) {
-                const uint32_t wi = load4(i), hi = hash3(wi);
-                const uint32_t nice = (len - i) < 258 ? (len - i) : 258;
-                int k = (int)R[i] - 1;
-                uint32_t best = 0, bestq = 0, wb = 0, s = 0;
-                for (; s < kPreCand && k >= 0; s++, k--) {
-                    const uint32_t q = S[k];
-                    const uint32_t wq = load4(q);
-                    // position 0 is zlib's NIL and the lowest position of its hash run
-                    if (q == 0 || hash3(wq) != hi) break;
-                    if (!may_beat(q, best, wb)) continue;
-                    const uint32_t cl = lcp(i, q, wi, wq, nice);
-                    if (cl > best) {
-                        best = cl;
-                        bestq = q;
-                        if (best >= nice) break;
-                        wb = best >= 4 ? load4(i + best - 3) : 0u;
-                    }
-                }
-                const bool cut = s == kPreCand && best < nice;
+        const uint32_t l = (uint32_t)lane_id();
+        uint32_t next = 64; // first unclaimed position (uniform)
+        uint32_t i = l, hi = 0, nice = 0, best = 0, bestq = 0, s = 0, c = 0, off = 0;
+        int k = -1;
+        bool ext = false, act = i < npos;
+        if (act) {
+            hi = hash3(load4(i));
+            nice = (len - i) < 258 ? (len - i) : 258;
+            k = (int)R[i] - 1;
+        }
+        while (ballot(act)) {
+            const bool fetch = act && !ext;
+            const bool can = fetch && k >= 0 && s < kPreCand;
+            const uint32_t qn = S[can ? k : 0];
+            c = ext ? c : qn;
+            off = ext ? off : 0u;
+            const uint32_t ii = act ? i : 0u;
+            const uint64_t A = load8(ii + off), B = load8(c + off);
+            const uint32_t bt = best >= 4 ? best - 3 : 0u;
+            const uint32_t Pi = load4(ii + bt), Pc = load4(c + bt);
+            // candidate fetch outcome (position 0 is zlib's NIL, the lowest entry of its run)
+            const bool ok = can && qn != 0 && hash3((uint32_t)B) == hi;
+            const bool chain_end = fetch && !ok;
+            const bool cut = chain_end && s >= kPreCand && best < nice;
+            const bool pruned = ok && best >= 4 && Pi != Pc;
+            const bool working = ext || (ok && !pruned);
+            const uint64_t y = A ^ B;
+            const uint32_t m = y ? (uint32_t)__builtin_ctzll(y) >> 3 : 8u;
+            const bool fin = working && (y != 0 || off + 8 >= nice);
+            uint32_t cl = off + m;
+            cl = cl < nice ? cl : nice;
+            const bool better = fin && cl > best;
+            best = better ? cl : best;
+            bestq = better ? c : bestq;
+            ext = working && !fin;
+            off = off + 8;
+            s += ok ? 1u : 0u;
+            k -= ok ? 1 : 0;
+            const bool done = act && (chain_end || (better && best >= nice));
+            const uint64_t dm = ballot(done);
+            if (done) {
                 M[i] = best | bestq << 9 | (cut ? 1u << 31 : 0u);
+                i = next + popc_lt(dm);
+                act = i < npos;
+                best = bestq = s = 0;
+                ext = false;
+                if (act) {
+                    hi = hash3(load4(i));
+                    nice = (len - i) < 258 ? (len - i) : 258;
+                    k = (int)R[i] - 1;
+                }
             }
+            next += (uint32_t)__builtin_popcountll(dm);
         }
         wave_sync();
     }
@@ -722,9 +763,11 @@ struct SmallWave {
         if (l == 0) lfreq[kEndBlock] = 1;
         wave_sync();
         stamp(6);
+        PMC_STOP(5, bitpos)
         TreeOut tl = build_tree(lfreq, kLCodes, TT.static_ltree, TT.extra_lbits, kLiterals + 1, kMaxBits, lcode);
         TreeOut td = build_tree(dfreq, kDCodes, TT.static_dtree, TT.extra_dbits, 0, kMaxBits, dcode);
         stamp(3);
+        PMC_STOP(6, bitpos)
         // (not in dad[]: the bit-length tree's build_tree below reuses dad[])
         PMC_LDS uint16_t *runL = runs, *runD = runs + 288;
         TreeOut tb{};
@@ -781,6 +824,7 @@ struct SmallWave {
             static_len = (int64_t)sl * 8 - 10;
         }
         stamp(7);
+        PMC_STOP(7, bitpos)
         const uint32_t opt_lenb_raw = (uint32_t)(((uint64_t)opt_len + 3 + 7) >> 3);
         const uint32_t static_lenb = (uint32_t)(((uint64_t)static_len + 3 + 7) >> 3);
         const uint32_t opt_lenb = static_lenb <= opt_lenb_raw ? static_lenb : opt_lenb_raw;
@@ -910,11 +954,14 @@ struct SmallWave {
         wave_sync();
         const uint32_t crc = wave_crc32(b, len, crc_tab);
         stamp(0);
+        PMC_STOP(1, 0)
         const uint32_t npos = len >= 3 ? len - 2 : 0;
         if (npos) {
             sort_positions(npos);
+            PMC_STOP(2, 0)
             match_all(npos, len);
         }
+        PMC_STOP(3, 0)
         stamp(1);
         // deflate_slow over the precomputed matches (single block: len < 16383 symbols).
         // M[] is read 64 entries at a time into a VGPR window and indexed with readlane, so a
@@ -965,6 +1012,7 @@ struct SmallWave {
         if ((ntok & 63) != 0 && (uint32_t)l < (ntok & 63)) tok[(ntok & ~63u) + l] = treg;
         wave_sync_global();
         stamp(2);
+        PMC_STOP(4, 0)
         // flush: the output image aliases the (dead) sort scratch
         for (uint64_t k = l; k < out_words; k += 64) outw[k] = 0;
         wave_sync();
@@ -975,6 +1023,10 @@ struct SmallWave {
         wave_sync();
         uint64_t bitpos = flush(ntok, len, 80);
         stamp(4);
+        PMC_STOP(5, 0)
+        PMC_STOP(6, 0)
+        PMC_STOP(7, 0)
+        PMC_STOP(8, 0)
         uint64_t nbytes = bitpos >> 3;
         if (l < 8) {
             uint32_t v = l < 4 ? crc : len;
@@ -1032,6 +1084,7 @@ __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
     w.fb = reinterpret_cast<Trees *>(a.scratch + wave * sizeof(Trees));
     w.crc_tab = to_lds<const uint32_t>(crc_tab);
     for (int k = 0; k < 16; k++) w.st[k] = 0;
+    w.stop = a.stop_after;
 #ifdef PMC_STAMPS
     w.t_last = __builtin_amdgcn_s_memtime();
 #endif

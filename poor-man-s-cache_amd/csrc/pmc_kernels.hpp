@@ -35,6 +35,7 @@ struct DeflateArgs {
     uint32_t *tokens;     // per-wave symbol slabs (kSlabSyms each)
     uint8_t *scratch;     // per-wave HBM working sets (HBM variant)
     uint64_t *dbg;        // PMC_STAMPS builds: per-phase cycle sums (else unused)
+    int32_t stop_after;   // PMC_STAMPS builds: end each value after phase k (cost attribution)
 };
 
 struct InflateArgs {
