@@ -39,7 +39,7 @@ struct SmallLayout {
     uint64_t out, lcode, dcode, blcode, dad, dep, runs, freq; // flush view
     uint64_t out_words;
     uint64_t T, cnt; // sort view
-    uint64_t M;      // parse view
+    uint64_t M, masks, masks_p; // parse view
 };
 
 __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
@@ -78,9 +78,11 @@ __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
     s += a(2 * n + 2);
     L.cnt = s;
     s += 16 * 64 * 2;
-    // parse view
+    // parse view: per-position match_all results, then the segment-walk bit masks
     L.M = L.X;
-    const uint64_t m = L.X + a(4 * n);
+    L.masks = L.M + a(4 * n);
+    L.masks_p = L.masks + a(((n + 63) / 64) * 8);
+    const uint64_t m = L.masks_p + a(((n + 63) / 64) * 8);
     uint64_t t = f > s ? f : s;
     t = t > m ? t : m;
     L.total = a(t);
@@ -213,7 +215,9 @@ struct SmallWave {
     PMC_LDS uint8_t *dep;
     PMC_LDS uint16_t *runs;
     PMC_LDS uint16_t *T, *H, *cnt;
-    PMC_LDS uint32_t *M; // per-position match_all results (aliases T/H after the sort)
+    PMC_LDS uint32_t *M;    // per-position match_all results (aliases the sort scratch)
+    PMC_LDS uint64_t *ML;   // segment walk: positions that start a match (or are unresolved)
+    PMC_LDS uint64_t *MP;   // segment walk: positions where a lazy-improvement run ends
     PMC_GLB uint32_t *tok;
     Trees *fb; // HBM scratch for the serial fallback
     PMC_LDS const uint32_t *crc_tab;
@@ -439,6 +443,115 @@ struct SmallWave {
         }
         *q_out = bestq;
         return best > b0 ? best : 0u;
+    }
+
+    // ---- deflate_slow as a walk over match segments ----------------------------------------
+    // From a fresh state at p (the start, or right after a match) zlib's lazy parse emits the
+    // literals [p, t) and then the match at t: j = the first position >= p whose match is
+    // usable, t = the end of the run of strict lazy improvements j, j+1, ... (each next
+    // position's match longer than the pending one, while it is < 258); the next fresh state
+    // is t + best_t.  Two bit masks built in parallel give j and t by find-first-set, so a
+    // segment costs a few scalar steps plus one vector store of its literal run.  A segment
+    // whose decisions touch a cut walk (M bit 31: longest_match not final) runs the exact
+    // step-by-step loop (with search()) up to its match instead.
+    __device__ void lit_run(uint32_t ntok, uint32_t p, uint32_t cnt) {
+        for (uint32_t k = (uint32_t)lane_id(); k < cnt; k += 64) tok[ntok + k] = p + k;
+    }
+    __device__ uint32_t ffs_mask(PMC_LDS const uint64_t *m, uint32_t from, uint32_t nw) const {
+        uint32_t w = from >> 6;
+        if (w >= nw) return 0xffffffffu;
+        uint64_t v = rfl64(m[w]) & (~0ull << (from & 63));
+        while (!v) {
+            if (++w >= nw) return 0xffffffffu;
+            v = rfl64(m[w]);
+        }
+        return w * 64 + (uint32_t)__builtin_ctzll(v);
+    }
+    __device__ __noinline__ uint32_t parse(uint32_t npos, uint32_t len) {
+        const uint32_t l = (uint32_t)lane_id();
+        const uint32_t nw = (npos + 63) >> 6;
+        for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+            const uint32_t j = c0 + l;
+            const uint32_t e = j < npos ? M[j] : 0u, e1 = j + 1 < npos ? M[j + 1] : 0u;
+            const uint32_t best = e & 511, q = (e >> 9) & 0x3fffu, best1 = e1 & 511;
+            const bool cut = (e >> 31) != 0;
+            const bool usable = best >= 4 || (best == 3 && j - q <= 4096); // TOO_FAR
+            const bool impr = best < 258 && j + 1 < npos && best1 > best;
+            const uint64_t mL = ballot(j < npos && (usable || cut));
+            const uint64_t mP = ballot(j < npos && (cut || !impr));
+            if (l == 0) {
+                ML[c0 >> 6] = mL;
+                MP[c0 >> 6] = mP;
+            }
+        }
+        wave_sync();
+        uint32_t p = 0, ntok = 0;
+        while (p < len) {
+            const uint32_t j = ffs_mask(ML, p, nw);
+            if (j == 0xffffffffu) { // no match ahead: literals to the end
+                lit_run(ntok, p, len - p);
+                ntok += len - p;
+                break;
+            }
+            const uint32_t ej = rfl(M[j]);
+            if (!(ej >> 31)) {
+                const uint32_t t = ffs_mask(MP, j, nw); // exists: bit npos-1 is always set
+                const uint32_t et = t == j ? ej : rfl(M[t]), bt = et & 511;
+                bool ok = !(et >> 31);
+                if (ok && bt < 258 && t + 1 < npos) {
+                    const uint32_t e1 = rfl(M[t + 1]);
+                    ok = !((e1 >> 31) && (e1 & 511) <= bt);
+                }
+                if (ok) {
+                    lit_run(ntok, p, t - p);
+                    ntok += t - p;
+                    if (l == 0) tok[ntok] = ((t - ((et >> 9) & 0x3fffu)) << 16) | (bt - 3);
+                    ntok++;
+                    p = t + bt;
+                    continue;
+                }
+            }
+            // exact step-by-step deflate_slow from the fresh state at p up to the next match
+            uint32_t i = p, match_length = 2, match_start = 0, prev_length, prev_match;
+            bool avail = false, matched = false;
+            while (i < len) {
+                prev_length = match_length;
+                prev_match = match_start;
+                match_length = 2;
+                if (i + 3 <= len && prev_length < 258) {
+                    const uint32_t e = rfl(M[i]);
+                    uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
+                    if (e >> 31) m = search(i, prev_length, len, m, q, &q);
+                    else if (m <= prev_length) m = 0;
+                    if (m) {
+                        match_length = m;
+                        match_start = q;
+                        if (m == 3 && i - q > 4096) match_length = 2;
+                    }
+                }
+                if (prev_length >= 3 && match_length <= prev_length) {
+                    if (l == 0) tok[ntok] = ((i - 1 - prev_match) << 16) | (prev_length - 3);
+                    ntok++;
+                    i += prev_length - 1;
+                    matched = true;
+                    break;
+                } else if (avail) {
+                    if (l == 0) tok[ntok] = i - 1;
+                    ntok++;
+                    i++;
+                } else {
+                    avail = true;
+                    i++;
+                }
+            }
+            if (!matched && avail) {
+                if (l == 0) tok[ntok] = i - 1;
+                ntok++;
+            }
+            p = i;
+        }
+        wave_sync_global();
+        return ntok;
     }
 
     // build_tree's heapify + merge loop (trees.c) on a register heap; returns the next
@@ -963,53 +1076,15 @@ struct SmallWave {
         }
         PMC_STOP(3, 0)
         stamp(1);
-        // deflate_slow over the precomputed matches (single block: len < 16383 symbols).
-        // M[] is read 64 entries at a time into a VGPR window and indexed with readlane, so a
-        // step costs scalar work only.  Tokens: match = (dist << 16) | (len - 3); literal =
-        // its position (dist 0), the byte is fetched in flush.
-        uint32_t i = 0, match_length = 2, prev_length, ntok = 0, treg = 0;
-        uint32_t match_start = 0, prev_match;
-        bool match_available = false;
-        uint32_t wbase = 0xffff0000u, wm = 0;
-        auto emit = [&](uint32_t token) {
-            if ((uint32_t)l == (ntok & 63)) treg = token;
-            if ((ntok & 63) == 63) tok[ntok - 63 + l] = treg;
-            ntok++;
-        };
-        while (i < len) {
-            prev_length = match_length;
-            prev_match = match_start;
-            match_length = 2;
-            if (i + 3 <= len && prev_length < 258) {
-                if (i - wbase >= 64) {
-                    wbase = i;
-                    wm = i + (uint32_t)l < npos ? M[i + l] : 0u;
-                }
-                const uint32_t e = readlane(wm, (int)(i - wbase));
-                uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
-                if (e >> 31) m = search(i, prev_length, len, m, q, &q);
-                else if (m <= prev_length) m = 0;
-                if (m) {
-                    match_length = m;
-                    match_start = q;
-                    if (m == 3 && i - q > 4096) match_length = 2;
-                }
-            }
-            if (prev_length >= 3 && match_length <= prev_length) {
-                emit(((i - 1 - prev_match) << 16) | (prev_length - 3));
-                i += prev_length - 1;
-                match_available = false;
-                match_length = 2;
-            } else if (match_available) {
-                emit(i - 1);
-                i++;
-            } else {
-                match_available = true;
-                i++;
-            }
+        // deflate_slow (single block: len < 16383 symbols).  Tokens: match = (dist << 16) |
+        // (len - 3); literal = its position (dist 0), the byte is fetched in flush.
+        uint32_t ntok;
+        if (npos) {
+            ntok = parse(npos, len);
+        } else { // no position with MIN_MATCH lookahead: all literals
+            lit_run(0, 0, len);
+            ntok = len;
         }
-        if (match_available) emit(i - 1);
-        if ((ntok & 63) != 0 && (uint32_t)l < (ntok & 63)) tok[(ntok & ~63u) + l] = treg;
         wave_sync_global();
         stamp(2);
         PMC_STOP(4, 0)
@@ -1080,6 +1155,8 @@ __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
     w.H = w.R; // hash keys live in R until the ranks overwrite them
     w.cnt = to_lds<uint16_t>(base + L.cnt);
     w.M = to_lds<uint32_t>(base + L.M);
+    w.ML = to_lds<uint64_t>(base + L.masks);
+    w.MP = to_lds<uint64_t>(base + L.masks_p);
     w.tok = (PMC_GLB uint32_t *)(a.tokens + wave * kSlabSyms);
     w.fb = reinterpret_cast<Trees *>(a.scratch + wave * sizeof(Trees));
     w.crc_tab = to_lds<const uint32_t>(crc_tab);

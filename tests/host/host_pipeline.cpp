@@ -384,7 +384,78 @@ int main(int argc, char **argv) {
     uint32_t match_length = 2, prev_length;
     uint64_t match_start = 0, prev_match;
     bool avail = false;
-    for (;;) {
+    if (pre) {
+        // v2 segment walk (pmc_deflate_small.hip parse()): from a fresh state at p, literals
+        // [p, t) then the match at t; segments touching a cut walk run the exact step loop.
+        auto best_of = [&](uint64_t j) { return j < npos ? M[j] & 511 : 0u; };
+        auto is_cut = [&](uint64_t j) { return j < npos && (M[j] >> 31); };
+        auto usable = [&](uint64_t j) {
+            uint32_t bj = best_of(j), q = (M[j] >> 9) & 0x3fff;
+            return bj >= 4 || (bj == 3 && j - q <= 4096);
+        };
+        auto stopL = [&](uint64_t j) { return j < npos && (usable(j) || is_cut(j)); };
+        auto stopP = [&](uint64_t j) {
+            bool impr = best_of(j) < 258 && j + 1 < npos && best_of(j + 1) > best_of(j);
+            return j < npos && (is_cut(j) || !impr);
+        };
+        uint64_t p = 0;
+        while (p < len) {
+            uint64_t j = p;
+            while (j < npos && !stopL(j)) j++;
+            if (j >= npos) {
+                for (uint64_t k = p; k < len; k++) emit(b[k]);
+                break;
+            }
+            if (!is_cut(j)) {
+                uint64_t t = j;
+                while (!stopP(t)) t++;
+                uint32_t bt = best_of(t);
+                bool ok = !is_cut(t);
+                if (ok && bt < 258 && t + 1 < npos) ok = !(is_cut(t + 1) && best_of(t + 1) <= bt);
+                if (ok) {
+                    for (uint64_t k = p; k < t; k++) emit(b[k]);
+                    emit((uint32_t)(t - ((M[t] >> 9) & 0x3fff)) << 16 | (bt - 3));
+                    p = t + bt;
+                    continue;
+                }
+            }
+            uint64_t ii = p;
+            uint32_t ml = 2;
+            uint64_t ms = 0;
+            bool av = false, matched = false;
+            while (ii < len) {
+                uint32_t pl = ml;
+                uint64_t pm = ms;
+                ml = 2;
+                if (ii + 3 <= len && pl < 258) {
+                    uint64_t q = 0;
+                    uint32_t m = search_pre(ii, pl, &q);
+                    if (m) {
+                        ml = m;
+                        ms = q;
+                        if (m == 3 && ii - q > 4096) ml = 2;
+                    }
+                }
+                if (pl >= 3 && ml <= pl) {
+                    emit((uint32_t)(ii - 1 - pm) << 16 | (pl - 3));
+                    ii += pl - 1;
+                    matched = true;
+                    break;
+                } else if (av) {
+                    emit(b[ii - 1]);
+                    ii++;
+                } else {
+                    av = true;
+                    ii++;
+                }
+            }
+            if (!matched && av) emit(b[ii - 1]);
+            p = ii;
+        }
+        i = len;
+        avail = false;
+    }
+    for (; !pre;) {
         if (wend - i < 262) {
             do {
                 if (i - B >= 32768 + 32506) B += 32768;
