@@ -144,24 +144,32 @@ __device__ __forceinline__ uint32_t s_sel_le(uint32_t a, uint32_t b, uint32_t t,
 }
 // Both small heaps keep every slot past heap_len (and slot 0) at ~0: a missing right child
 // then never wins the smaller() test, so no j < heap_len check is needed.
+// pqdownheap in three steps: (1) every parent lane computes its smaller child at once (zlib's
+// smaller(): the right child wins ties), packed key << 8 | child index; (2) the scalar walk
+// follows those links from k with one v_readlane + compare per level, collecting the path
+// (the smaller children along a sift path are not changed by the sift, so this is exact);
+// (3) every path entry takes its smaller child's value in one parallel select.
 struct RegHeap1 {
     uint32_t h;
     __device__ uint32_t get(int k) const { return readlane(h, k); }
     __device__ void set(int k, uint32_t v) { h = writelane(h, v, k); }
     __device__ void down(int k, int n) {
+        const int l = lane_id();
         const uint32_t v = readlane(h, k), kv = v >> 10;
-        int j = k << 1;
-        while (j <= n) {
-            const uint32_t x0 = readlane(h, j), y = readlane(h, (j + 1) & 63);
-            const uint32_t kx = x0 >> 10, ky = y >> 10;
-            const uint32_t x = s_sel_le(ky, kx, y, x0);
-            const int jn = (int)s_sel_le(ky, kx, (uint32_t)j + 1, (uint32_t)j);
-            if (kv <= (x >> 10)) break;
-            h = writelane(h, x, k);
-            k = jn;
-            j = k << 1;
+        const uint32_t a = (uint32_t)__shfl((int)h, (2 * l) & 63), b = (uint32_t)__shfl((int)h, (2 * l + 1) & 63);
+        const bool right = (b >> 10) <= (a >> 10);
+        const uint32_t mv = right ? b : a;
+        const uint32_t pk = (mv >> 10) << 8 | (uint32_t)(2 * l + (right ? 1 : 0));
+        uint64_t path = 0;
+        int cur = k;
+        while (2 * cur <= n) {
+            const uint32_t e = readlane(pk, cur);
+            if (kv <= (e >> 8)) break;
+            path |= 1ull << cur;
+            cur = (int)(e & 0xff);
         }
-        h = writelane(h, v, k);
+        h = ((path >> l) & 1) ? mv : h;
+        h = writelane(h, v, cur);
     }
 };
 struct RegHeap2 {
@@ -177,19 +185,28 @@ struct RegHeap2 {
         h1 = (hit & odd) ? v : h1;
     }
     __device__ void down(int k, int n) {
+        const int l = lane_id();
         const uint32_t v = get(k), kv = v >> 10;
-        int j = k << 1;
-        while (j <= n) {
-            const uint32_t x0 = readlane(h0, k), y = readlane(h1, k);
-            const uint32_t kx = x0 >> 10, ky = y >> 10;
-            const uint32_t x = s_sel_le(ky, kx, y, x0);
-            const int jn = (int)s_sel_le(ky, kx, (uint32_t)j + 1, (uint32_t)j);
-            if (kv <= (x >> 10)) break;
-            set(k, x);
-            k = jn;
-            j = k << 1;
+        // lane p holds the children 2p (h0) and 2p+1 (h1) of entry p
+        const bool right = (h1 >> 10) <= (h0 >> 10);
+        const uint32_t mv = right ? h1 : h0;
+        const uint32_t pk = (mv >> 10) << 8 | (uint32_t)(2 * l + (right ? 1 : 0));
+        uint64_t p0 = 0, p1 = 0; // path entries 2L (bit L of p0) and 2L+1 (bit L of p1)
+        int cur = k;
+        while (2 * cur <= n) {
+            const uint32_t e = readlane(pk, cur);
+            if (kv <= (e >> 8)) break;
+            if (cur & 1) p1 |= 1ull << (cur >> 1);
+            else p0 |= 1ull << (cur >> 1);
+            cur = (int)(e & 0xff);
         }
-        set(k, v);
+        if (p0 | p1) { // entry p (lane p>>1 of h[p&1]) takes mv of lane p
+            const uint32_t s0 = (uint32_t)__shfl((int)mv, (2 * l) & 63);
+            const uint32_t s1 = (uint32_t)__shfl((int)mv, (2 * l + 1) & 63);
+            h0 = ((p0 >> l) & 1) ? s0 : h0;
+            h1 = ((p1 >> l) & 1) ? s1 : h1;
+        }
+        set(cur, v);
     }
 };
 
