@@ -712,10 +712,11 @@ struct InflateLds {
         de = T->dfast[bits & ((1u << kRootBits) - 1)];
     }
 
-    // write the batch's tokens: literals in one store, then matches in stream order
-    __device__ void materialise(uint32_t nt, uint32_t tokv, uint32_t tposv, uint32_t o0, uint32_t cap) {
+    // write the tokens of the lanes in `act` (stream order = lane order): literals in one
+    // store, then matches one after another (a match may read bytes the previous one wrote)
+    __device__ void materialise(uint64_t actm, uint32_t tokv, uint32_t tposv, uint32_t o0, uint32_t cap) {
         const uint32_t l = (uint32_t)lane_id();
-        const bool act = l < nt;
+        const bool act = (actm >> l) & 1;
         const uint32_t p = o0 + tposv;
         if (act && !(tokv >> 31) && p < cap) out[p] = (uint8_t)tokv;
         uint64_t mm = ballot(act && (tokv >> 31));
@@ -739,6 +740,61 @@ struct InflateLds {
             }
         }
         wave_sync();
+    }
+
+    // Exact decode of the one token at bit W, with inflate.c's checks in its order.  Returns
+    // 0 (token in tok/olen, W advanced), 1 (end of block, W advanced) or a verdict < 0.
+    __device__ int scalar_token(uint32_t &W, uint32_t o, uint32_t nbits, uint32_t lcnt, uint32_t dcnt,
+                                uint32_t &tok, uint32_t &olen) {
+        uint32_t bits, le, de;
+        window(W, bits, le, de);
+        const uint32_t e = readlane(le, 0);
+        uint32_t L, sym;
+        if (e < kEntInvalid) {
+            L = e >> 9;
+            sym = e & 0x1ff;
+        } else if (e == kEntInvalid) {
+            return W + 1 > nbits ? PMC_Z_BUF_ERROR_DEV : PMC_Z_DATA_ERROR_DEV;
+        } else {
+            sym = slow_decode(readlane(bits, 0), lcnt, T->lsym, L);
+        }
+        if (W + L > nbits) return PMC_Z_BUF_ERROR_DEV;
+        if (sym < 256) {
+            tok = sym;
+            olen = 1;
+            W += L;
+            return 0;
+        }
+        if (sym == 256) {
+            W += L;
+            return 1;
+        }
+        const uint32_t s = sym - 257;
+        if (s >= 29) return PMC_Z_DATA_ERROR_DEV;
+        const uint32_t lv = readlane(lenv, (int)s), eb = lv >> 16;
+        if (W + L + eb > nbits) return PMC_Z_BUF_ERROR_DEV;
+        const uint32_t mlen = (lv & 0xffff) + ((readlane(bits, 0) >> L) & ((1u << eb) - 1));
+        const uint32_t x = L + eb; // <= 20: the distance code starts inside this window
+        const uint32_t f = readlane(de, (int)x);
+        uint32_t dL, ds;
+        if (f < kEntInvalid) {
+            dL = f >> 9;
+            ds = f & 0x1ff;
+        } else if (f == kEntInvalid) {
+            return W + x + 1 > nbits ? PMC_Z_BUF_ERROR_DEV : PMC_Z_DATA_ERROR_DEV;
+        } else {
+            ds = slow_decode(readlane(bits, (int)x), dcnt, T->dsym, dL);
+        }
+        if (W + x + dL > nbits) return PMC_Z_BUF_ERROR_DEV;
+        if (ds >= 30) return PMC_Z_DATA_ERROR_DEV;
+        const uint32_t dv = readlane(distv, (int)ds), deb = dv >> 16;
+        if (W + x + dL + deb > nbits) return PMC_Z_BUF_ERROR_DEV;
+        const uint32_t dist = (dv & 0xffff) + ((readlane(bits, (int)x) >> dL) & ((1u << deb) - 1));
+        if (dist > o) return PMC_Z_DATA_ERROR_DEV;
+        tok = 0x80000000u | (dist - 1) << 8 | (mlen - 3);
+        olen = mlen;
+        W += x + dL + deb;
+        return 0;
     }
 
     __device__ int run(const uint8_t *src, uint32_t in_len, uint8_t *dst, uint32_t cap, uint32_t *dst_len) {
@@ -920,90 +976,73 @@ struct InflateLds {
                     return PMC_Z_DATA_ERROR_DEV;
                 stamp(2);
             }
-            // ---- symbols: windowed speculative decode, batches of <= 64 tokens ----
-            uint32_t W = sb.pos(), x = 0, bits, le, de;
-            window(W, bits, le, de);
-            uint32_t pend = 0; // pending match length (its distance not decoded yet)
+            // ---- symbols: every lane decodes a whole token at its offset W + lane of a window,
+            // a scalar chase follows the next-token links, the path's tokens are written at once
+            uint32_t W = sb.pos();
             for (;;) {
-                uint32_t nt = 0, tokv = 0, tposv = 0;
-                const uint32_t o0 = o;
-                int stt = 0;
-                while (nt < 64) {
-                    if (x >= 64) {
-                        W += x;
-                        x = 0;
-                        window(W, bits, le, de);
+                uint32_t bits, le, de;
+                window(W, bits, le, de);
+                const uint32_t ul = (uint32_t)l;
+                const bool lok = le < kEntInvalid;
+                const uint32_t L = (le >> 9) & 31, sym = le & 0x1ff, s = (sym - 257) & 31;
+                const bool islit = lok && sym < 256, iseob = lok && sym == 256;
+                const bool islen = lok && sym > 256 && sym < 286;
+                const uint32_t lv = (uint32_t)__shfl((int)lenv, (int)s), eb = lv >> 16;
+                const uint32_t mlen = (lv & 0xffff) + ((bits >> L) & ((1u << eb) - 1));
+                const uint32_t x2 = ul + L + eb;
+                const uint32_t dde = (uint32_t)__shfl((int)de, (int)(x2 & 63));
+                const uint32_t dbits = (uint32_t)__shfl((int)bits, (int)(x2 & 63));
+                const uint32_t dL = (dde >> 9) & 31, ds = dde & 0x1ff;
+                const bool dok = dde < kEntInvalid && ds < 30;
+                const uint32_t dv = (uint32_t)__shfl((int)distv, (int)(ds & 31)), deb = dv >> 16;
+                const uint32_t dist = (dv & 0xffff) + ((dbits >> dL) & ((1u << deb) - 1));
+                const uint32_t nxt = islen ? x2 + dL + deb : ul + L;
+                const bool partial = islen && x2 >= 64;
+                const bool fast = (islit || iseob || (islen && !partial && dok)) && W + nxt <= nbits;
+                // info: next offset | 0x100 exact path needed | 0x200 end of block | 0x400 re-window
+                const uint32_t info =
+                    nxt | (partial ? 0x400u : fast ? (iseob ? 0x200u : 0u) : 0x100u);
+                const uint32_t tok = islit ? sym : (0x80000000u | (dist - 1) << 8 | (mlen - 3));
+                uint64_t path = 0;
+                uint32_t x = 0, stop = 0;
+                while (x < 64) {
+                    const uint32_t f = readlane(info, (int)x);
+                    if (f & 0x700) {
+                        stop = f;
+                        break;
                     }
-                    const uint32_t pos = W + x;
-                    if (pend == 0) {
-                        const uint32_t e = readlane(le, (int)x);
-                        uint32_t L, sym;
-                        if (e < kEntInvalid) {
-                            L = e >> 9;
-                            sym = e & 0x1ff;
-                        } else if (e == kEntInvalid) {
-                            stt = pos + 1 > nbits ? PMC_Z_BUF_ERROR_DEV : PMC_Z_DATA_ERROR_DEV;
-                            break;
-                        } else {
-                            sym = slow_decode(readlane(bits, (int)x), lcnt, T->lsym, L);
-                        }
-                        if (pos + L > nbits) { stt = PMC_Z_BUF_ERROR_DEV; break; }
-                        if (sym < 256) {
-                            if ((uint32_t)l == nt) {
-                                tokv = sym;
-                                tposv = o - o0;
-                            }
-                            nt++;
-                            o++;
-                            x += L;
-                            continue;
-                        }
-                        if (sym == 256) {
-                            x += L;
-                            stt = 1;
-                            break;
-                        }
-                        const uint32_t s = sym - 257;
-                        if (s >= 29) { stt = PMC_Z_DATA_ERROR_DEV; break; }
-                        const uint32_t lv = readlane(lenv, (int)s), eb = lv >> 16;
-                        if (pos + L + eb > nbits) { stt = PMC_Z_BUF_ERROR_DEV; break; }
-                        pend = (lv & 0xffff) + ((readlane(bits, (int)x) >> L) & ((1u << eb) - 1));
-                        x += L + eb;
-                    } else {
-                        const uint32_t e = readlane(de, (int)x);
-                        uint32_t L, ds;
-                        if (e < kEntInvalid) {
-                            L = e >> 9;
-                            ds = e & 0x1ff;
-                        } else if (e == kEntInvalid) {
-                            stt = pos + 1 > nbits ? PMC_Z_BUF_ERROR_DEV : PMC_Z_DATA_ERROR_DEV;
-                            break;
-                        } else {
-                            ds = slow_decode(readlane(bits, (int)x), dcnt, T->dsym, L);
-                        }
-                        if (pos + L > nbits) { stt = PMC_Z_BUF_ERROR_DEV; break; }
-                        if (ds >= 30) { stt = PMC_Z_DATA_ERROR_DEV; break; }
-                        const uint32_t dv = readlane(distv, (int)ds), eb = dv >> 16;
-                        if (pos + L + eb > nbits) { stt = PMC_Z_BUF_ERROR_DEV; break; }
-                        const uint32_t dist = (dv & 0xffff) + ((readlane(bits, (int)x) >> L) & ((1u << eb) - 1));
-                        if (dist > o) { stt = PMC_Z_DATA_ERROR_DEV; break; }
-                        if ((uint32_t)l == nt) {
-                            tokv = 0x80000000u | (dist - 1) << 8 | (pend - 3);
-                            tposv = o - o0;
-                        }
-                        nt++;
-                        o += pend;
-                        pend = 0;
-                        x += L + eb;
-                    }
+                    path |= 1ull << x;
+                    x = f & 0xff;
                 }
                 stamp(3);
-                materialise(nt, tokv, tposv, o0, cap);
+                if (path) {
+                    const bool on = (path >> ul) & 1;
+                    const uint32_t ol = on ? (islit ? 1u : mlen) : 0u;
+                    const uint32_t incl = wave_incl_scan_dpp(ol), tpos = incl - ol;
+                    if (ballot(on && islen && dist > o + tpos)) return PMC_Z_DATA_ERROR_DEV;
+                    materialise(path, tok, tpos, o, cap);
+                    o += readlane(incl, 63);
+                }
                 stamp(4);
-                if (stt < 0) return stt;
-                if (stt == 1) break;
+                if (x >= 64 || (stop & 0x400)) { // window used up / a match's distance lies past it
+                    W += x;
+                    continue;
+                }
+                if (stop & 0x200) { // end of block
+                    W += stop & 0xff;
+                    break;
+                }
+                // exact single-token decode (code longer than the root, invalid code, truncation)
+                W += x;
+                uint32_t t1 = 0, n1 = 0;
+                const int r1 = scalar_token(W, o, nbits, lcnt, dcnt, t1, n1);
+                if (r1 < 0) return r1;
+                if (r1 == 1) break;
+                materialise(1ull, l == 0 ? t1 : 0u, 0u, o, cap);
+                o += n1;
+                stamp(3);
             }
-            sb.seek(W + x);
+            sb.seek(W);
         } while (!last);
         // 3. trailer: CRC-32 then ISIZE (inflate.c CHECK / LENGTH)
         const uint32_t tp = (sb.pos() + 7) >> 3;
