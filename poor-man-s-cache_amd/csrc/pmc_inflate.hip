@@ -984,19 +984,25 @@ struct InflateLds {
                 window(W, bits, le, de);
                 const uint32_t ul = (uint32_t)l;
                 const bool lok = le < kEntInvalid;
-                const uint32_t L = (le >> 9) & 31, sym = le & 0x1ff, s = (sym - 257) & 31;
+                const uint32_t L = (le >> 9) & 31, sym = le & 0x1ff, s = sym - 257;
                 const bool islit = lok && sym < 256, iseob = lok && sym == 256;
                 const bool islen = lok && sym > 256 && sym < 286;
-                const uint32_t lv = (uint32_t)__shfl((int)lenv, (int)s), eb = lv >> 16;
-                const uint32_t mlen = (lv & 0xffff) + ((bits >> L) & ((1u << eb) - 1));
+                // length base / extra bits in closed form (inflate.c lbase / lext)
+                const uint32_t eb = (s >= 8 && s < 28) ? (s >> 2) - 1 : 0u;
+                const uint32_t lbase = s < 8 ? s + 3 : s == 28 ? 258u : ((4 + (s & 3)) << eb) + 3;
+                const uint32_t mlen = lbase + ((bits >> L) & ((1u << eb) - 1));
                 const uint32_t x2 = ul + L + eb;
-                const uint32_t dde = (uint32_t)__shfl((int)de, (int)(x2 & 63));
-                const uint32_t dbits = (uint32_t)__shfl((int)bits, (int)(x2 & 63));
-                const uint32_t dL = (dde >> 9) & 31, ds = dde & 0x1ff;
-                const bool dok = dde < kEntInvalid && ds < 30;
-                const uint32_t dv = (uint32_t)__shfl((int)distv, (int)(ds & 31)), deb = dv >> 16;
-                const uint32_t dist = (dv & 0xffff) + ((dbits >> dL) & ((1u << deb) - 1));
-                const uint32_t nxt = islen ? x2 + dL + deb : ul + L;
+                // every lane also decodes "a distance code starting here" (inflate.c dbase / dext),
+                // packed dist | bits used << 16 | bad << 31, and the length lane fetches lane x2's
+                const uint32_t dL = (de >> 9) & 31, ds = de & 0x1ff;
+                const bool dok0 = de < kEntInvalid && ds < 30;
+                const uint32_t deb = ds >= 4 ? (ds >> 1) - 1 : 0u;
+                const uint32_t dbase = ds < 4 ? ds + 1 : ((2 + (ds & 1)) << deb) + 1;
+                const uint32_t dpk = dok0 ? (dbase + ((bits >> dL) & ((1u << deb) - 1))) | (dL + deb) << 16 : 0x80000000u;
+                const uint32_t dg = (uint32_t)__shfl((int)dpk, (int)(x2 & 63));
+                const bool dok = !(dg >> 31);
+                const uint32_t dist = dg & 0xffff;
+                const uint32_t nxt = islen ? x2 + ((dg >> 16) & 0xff) : ul + L;
                 const bool partial = islen && x2 >= 64;
                 const bool fast = (islit || iseob || (islen && !partial && dok)) && W + nxt <= nbits;
                 // info: next offset | 0x100 exact path needed | 0x200 end of block | 0x400 re-window
@@ -1073,7 +1079,7 @@ struct InflateLds {
 };
 
 template <bool kHbm>
-__global__ void __launch_bounds__(256) inflate_kernel(InflateArgs a) {
+__global__ void __launch_bounds__(256, 5) inflate_kernel(InflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
     for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
