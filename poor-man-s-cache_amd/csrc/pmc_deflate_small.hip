@@ -249,6 +249,11 @@ struct SmallWave {
         t_last = t;
 #endif
     }
+    __device__ void count(int k) {
+#ifdef PMC_STAMPS
+        st[k]++;
+#endif
+    }
 #ifdef PMC_STAMPS
 #define PMC_STOP(k, ret)                                                                                               \
     if (stop == (k)) return ret;
@@ -528,9 +533,16 @@ struct SmallWave {
                     continue;
                 }
             }
-            // exact step-by-step deflate_slow from the fresh state at p up to the next match
-            uint32_t i = p, match_length = 2, match_start = 0, prev_length, prev_match;
-            bool avail = false, matched = false;
+            // exact step-by-step deflate_slow up to the next match.  Positions [p, j) have no
+            // usable match (and no cut walk), so the fresh state at p reaches j having emitted
+            // the literals [p, j - 1) with b[j - 1] pending (when j > p) and match_length 2.
+            stamp(2);
+            if (j > p + 1) {
+                lit_run(ntok, p, j - 1 - p);
+                ntok += j - 1 - p;
+            }
+            uint32_t i = j, match_length = 2, match_start = 0, prev_length, prev_match;
+            bool avail = j > p, matched = false;
             while (i < len) {
                 prev_length = match_length;
                 prev_match = match_start;
@@ -538,7 +550,10 @@ struct SmallWave {
                 if (i + 3 <= len && prev_length < 258) {
                     const uint32_t e = rfl(M[i]);
                     uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
-                    if (e >> 31) m = search(i, prev_length, len, m, q, &q);
+                    if (e >> 31) {
+                        m = search(i, prev_length, len, m, q, &q);
+                        count(15);
+                    }
                     else if (m <= prev_length) m = 0;
                     if (m) {
                         match_length = m;
@@ -566,6 +581,7 @@ struct SmallWave {
                 ntok++;
             }
             p = i;
+            stamp(14);
         }
         wave_sync_global();
         return ntok;
@@ -1088,6 +1104,7 @@ struct SmallWave {
         const uint32_t npos = len >= 3 ? len - 2 : 0;
         if (npos) {
             sort_positions(npos);
+            stamp(13);
             PMC_STOP(2, 0)
             match_all(npos, len);
         }

@@ -15,9 +15,10 @@ import torch  # noqa: E402
 import pmc_codec  # noqa: E402
 from pmc_codec import device as D  # noqa: E402
 
-PHASES = ["stage+crc", "hash+sort+match_all", "parse", "trees lit+dist (rest)", "emit", "trailer+copy",
-          "zero+histogram", "runs+bl tree (rest)", "bt:leaves", "bt:heap", "bt:depths", "bt:sums", "bt:codes", "-",
-          "-", "-"]
+PHASES = ["stage+crc", "match_all", "parse", "trees lit+dist (rest)", "emit", "trailer+copy",
+          "zero+histogram", "runs+bl tree (rest)", "bt:leaves", "bt:heap", "bt:depths", "bt:sums", "bt:codes", "hash+sort",
+          "parse:exact+search", "#search calls"]
+COUNTS = {15}
 IPHASES = ["inf:stage+header", "inf:block hdr+code lens", "inf:table builds", "inf:symbol decode",
            "inf:materialise", "inf:crc+copy", "-", "-"]
 
@@ -44,12 +45,13 @@ def main():
         torch.cuda.synchronize()
         s = dbg.cpu().tolist()
         for lo, names, what in ((0, PHASES, "deflate"), (16, IPHASES, "inflate")):
-            tot = sum(s[lo:lo + 16])
+            tot = sum(v for k, v in enumerate(s[lo:lo + 16]) if lo or k not in COUNTS)
             bad = int((rc != 0).sum()) if lo == 0 else int((brc != 0).sum())
             print(f"vlen={vlen} kind={kind} n={n} {what}: wave-cycles/value total {tot / n:,.0f}  rc!=0: {bad}")
             for k, name in enumerate(names):
                 if s[lo + k]:
-                    print(f"   {name:24s} {s[lo + k] / n:12,.0f}  {100 * s[lo + k] / tot:5.1f}%")
+                    pct = "" if (lo == 0 and k in COUNTS) else f"{100 * s[lo + k] / tot:5.1f}%"
+                    print(f"   {name:24s} {s[lo + k] / n:12,.1f}  {pct}")
     ctx.close()
 
 

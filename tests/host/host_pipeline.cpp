@@ -419,10 +419,12 @@ int main(int argc, char **argv) {
                     continue;
                 }
             }
-            uint64_t ii = p;
+            // positions [p, j) have no usable match: literals [p, j - 1), b[j - 1] pending
+            for (uint64_t k = p; k + 1 < j; k++) emit(b[k]);
+            uint64_t ii = j;
             uint32_t ml = 2;
             uint64_t ms = 0;
-            bool av = false, matched = false;
+            bool av = j > p, matched = false;
             while (ii < len) {
                 uint32_t pl = ml;
                 uint64_t pm = ms;
