@@ -218,6 +218,9 @@ struct TreeOut {
 };
 
 #define PMC_GLB __attribute__((address_space(1)))
+#ifndef PMC_GROUP
+#define PMC_GROUP 2
+#endif
 struct SmallWave {
     // every working array is LDS-typed (ds_* with 32-bit addresses)
     PMC_LDS uint8_t *b;
@@ -233,6 +236,7 @@ struct SmallWave {
     PMC_LDS uint16_t *runs;
     PMC_LDS uint16_t *T, *H, *cnt;
     PMC_LDS uint32_t *M;    // per-position match_all results (aliases the sort scratch)
+    PMC_LDS uint64_t *HC;   // on-demand parse: bit x = position x has a chain candidate (aliases M)
     PMC_LDS uint64_t *ML;   // segment walk: positions that start a match (or are unresolved)
     PMC_LDS uint64_t *MP;   // segment walk: positions where a lazy-improvement run ends
     PMC_GLB uint32_t *tok;
@@ -354,7 +358,10 @@ struct SmallWave {
     // parallel before the serial parse.  M[i] = best | bestq << 9 | (walk cut short) << 31
     // with best = max over those candidates of min(LCP, nice), bestq the nearest achieving
     // it.  A cut-short walk is finished by search() if the parse visits i.
-    static constexpr uint32_t kPreCand = 16;
+    // on-demand evaluation: kGroup positions per wave step, kPreCand = 64 / kGroup chain
+    // candidates per position (one lane each)
+    static constexpr uint32_t kGroup = PMC_GROUP;
+    static constexpr uint32_t kPreCand = 64 / kGroup;
     // Work-stealing walk, branch-light: every iteration each lane issues the same loads
     // (one chain entry, 8 bytes at i+off and at c+off, the two prune words) and advances
     // its state with selects -- a candidate is fetched, pruned, or compared 8 bytes further.
@@ -585,6 +592,247 @@ struct SmallWave {
         }
         wave_sync_global();
         return ntok;
+    }
+
+    // ---- deflate_slow with on-demand longest_match ------------------------------------------
+    // Only positions the lazy parse visits need longest_match (about 15 % of the positions of
+    // a 1 KiB JSON value that have chain candidates at all).  The parse runs serially on the
+    // scalar unit; whenever it reaches a position with candidates whose result is not at hand,
+    // one wave step evaluates that position and the next kGroup - 1 positions with candidates:
+    // each lane compares one (position, candidate) pair -- candidates 1..kPreCand of the chain,
+    // nearest first -- and a DPP row max picks (longest, then nearest).  A chain with more than
+    // kPreCand candidates is finished by search() when the parse uses it.  Positions without
+    // candidates (HC bit clear) are skipped in bulk as literals.
+    __device__ void build_hc(uint32_t npos) {
+        const uint32_t l = (uint32_t)lane_id();
+        for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+            const uint32_t x = c0 + l;
+            bool v = x < npos;
+            const uint32_t r = v ? R[x] : 0u;
+            v = v && r >= 1;
+            const uint32_t q = v ? S[r - 1] : 0u;
+            v = v && q != 0 && hash3(load4(q)) == hash3(load4(x));
+            const uint64_t m = ballot(v);
+            if (l == 0) HC[c0 >> 6] = m;
+        }
+        wave_sync();
+    }
+    // results of the current group: position (or ~0) and best | q << 9 | cut << 31
+    struct Group {
+        uint32_t p[kGroup], e[kGroup];
+    };
+    __device__ void eval_group(Group &g, uint32_t p0, uint32_t npos, uint32_t len) {
+        const uint32_t l = (uint32_t)lane_id(), nw = (npos + 63) >> 6;
+        g.p[0] = p0;
+#pragma unroll
+        for (uint32_t r = 1; r < kGroup; r++)
+            g.p[r] = g.p[r - 1] == 0xffffffffu ? 0xffffffffu : ffs_mask(HC, g.p[r - 1] + 1, nw);
+        const uint32_t row = l / kPreCand, d = l % kPreCand + 1;
+        uint32_t P = g.p[0];
+#pragma unroll
+        for (uint32_t r = 1; r < kGroup; r++) P = row == r ? g.p[r] : P;
+        bool v = P != 0xffffffffu;
+        P = v ? P : 0u;
+        const int k = v ? (int)R[P] - (int)d : -1;
+        v = k >= 0;
+        const uint32_t q = v ? S[k] : 0u;
+        v = v && q != 0;
+        const uint64_t A = load8(P), B = load8(q);
+        v = v && hash3((uint32_t)A) == hash3((uint32_t)B);
+        const uint32_t nice = (len - P) < 258 ? (len - P) : 258;
+        const uint64_t y = A ^ B;
+        uint32_t cl = y ? (uint32_t)__builtin_ctzll(y) >> 3 : 8u;
+        bool ext = v && y == 0 && nice > 8;
+        uint32_t off = 8;
+        while (ballot(ext)) {
+            count(13);
+            const uint64_t y2 = load8(ext ? P + off : 0u) ^ load8(ext ? q + off : 0u);
+            cl = ext ? (y2 ? off + ((uint32_t)__builtin_ctzll(y2) >> 3) : off + 8) : cl;
+            ext = ext && y2 == 0 && off + 8 < nice;
+            off += 8;
+        }
+        cl = cl < nice ? cl : nice;
+        uint32_t key = v ? (cl << 23 | (kPreCand - d) << 18 | q) : 0u;
+        key = dpp_row_max(key);
+        const uint64_t vm = ballot(v);
+        uint32_t rk[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) rk[r] = readlane(key, 16 * r);
+#pragma unroll
+        for (uint32_t r = 0; r < kGroup; r++) {
+            uint32_t kk = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4 / kGroup; j++) {
+                const uint32_t x = rk[r * (4 / kGroup) + j];
+                kk = x > kk ? x : kk;
+            }
+            const uint64_t rowm = (vm >> (r * kPreCand)) & (kPreCand == 64 ? ~0ull : ((1ull << kPreCand) - 1));
+            const uint32_t best = kk >> 23, pr = g.p[r];
+            const uint32_t nice_r = (len - pr) < 258 ? (len - pr) : 258;
+            const bool full = rowm == (kPreCand == 64 ? ~0ull : ((1ull << kPreCand) - 1));
+            g.e[r] = best | (kk & 0x3fffu) << 9 | ((full && best < nice_r) ? 1u << 31 : 0u);
+        }
+    }
+    // Token sink: tokens collect in one VGPR (lane k holds token 64 * block + k) and leave
+    // with one coalesced store per 64 tokens, so emitting costs no exec-masked stores.
+    struct TokBuf {
+        uint32_t v = 0, n = 0;
+    };
+    __device__ void tb_flush(TokBuf &t) { tok[t.n - 64 + (uint32_t)lane_id()] = t.v; }
+    __device__ void tb_put(TokBuf &t, uint32_t x) {
+        t.v = (uint32_t)lane_id() == (t.n & 63) ? x : t.v;
+        t.n++;
+        if ((t.n & 63) == 0) tb_flush(t);
+    }
+    // literal tokens for positions p .. p + cnt - 1
+    __device__ void tb_run(TokBuf &t, uint32_t p, uint32_t cnt) {
+        const uint32_t l = (uint32_t)lane_id();
+        while (cnt) {
+            const uint32_t o = t.n & 63, take = cnt < 64 - o ? cnt : 64 - o;
+            t.v = l - o < take ? p + (l - o) : t.v;
+            t.n += take;
+            p += take;
+            cnt -= take;
+            if ((t.n & 63) == 0) tb_flush(t);
+        }
+    }
+    __device__ void tb_finish(TokBuf &t) {
+        const uint32_t l = (uint32_t)lane_id();
+        if (l < (t.n & 63)) tok[(t.n & ~63u) + l] = t.v;
+    }
+    // longest_match record of has-candidate position x (evaluating a new group if needed)
+    __device__ uint32_t group_get(Group &g, uint32_t x, uint32_t npos, uint32_t len) {
+        uint32_t e = 0xffffffffu;
+#pragma unroll
+        for (uint32_t r = 0; r < kGroup; r++) e = g.p[r] == x ? g.e[r] : e;
+        if (e == 0xffffffffu) {
+            eval_group(g, x, npos, len);
+#pragma unroll
+            for (uint32_t r = 0; r < kGroup; r++) {
+                g.p[r] = rfl(g.p[r]);
+                g.e[r] = rfl(g.e[r]);
+            }
+            e = g.e[0];
+        }
+        return e;
+    }
+    __device__ __noinline__ uint32_t parse_ondemand(uint32_t npos_, uint32_t len_) {
+        const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
+        const uint32_t nw = (npos + 63) >> 6;
+        build_hc(npos);
+        Group g;
+#pragma unroll
+        for (uint32_t r = 0; r < kGroup; r++) g.p[r] = 0xffffffffu;
+        TokBuf tb;
+        uint32_t i = 0, ml = 2, ms = 0, av = 0;
+        uint32_t hci = 0;              // HC word cached in SGPRs
+        uint64_t hcw = rfl64(HC[0]);
+        while (i < len) {
+            // (the parse state is wave-uniform: keep it in SGPRs so control stays scalar)
+            i = rfl(i);
+            ml = rfl(ml);
+            ms = rfl(ms);
+            av = rfl(av);
+            tb.n = rfl(tb.n);
+            if (ml == 2) {
+                // no pending match: positions without chain candidates only pass the pending
+                // literal on, so jump to the next position that has candidates
+                uint32_t j = len;
+                uint32_t w = i >> 6;
+                if (w < nw) {
+                    if (w != hci) {
+                        hci = w;
+                        hcw = rfl64(HC[w]);
+                    }
+                    uint64_t m = hcw & (~0ull << (i & 63));
+                    while (!m && ++w < nw) {
+                        hci = w;
+                        hcw = rfl64(HC[w]);
+                        m = hcw;
+                    }
+                    if (m) j = w * 64 + (uint32_t)__builtin_ctzll(m);
+                }
+                if (j > i) {
+                    const uint32_t from = av ? i - 1 : i;
+                    tb_run(tb, from, j - 1 - from);
+                    av = 1;
+                    i = j;
+                    if (i >= len) break;
+                }
+                // fast path at a has-candidate position i with no pending match (i < npos):
+                // an unusable result is a literal step; a usable one that position i + 1 does
+                // not improve on is emitted at once.  Cut walks and lazy improvements take the
+                // general step below.
+                if (i < npos) {
+                    const uint32_t e0 = group_get(g, i, npos, len);
+                    if (!(e0 >> 31)) {
+                        const uint32_t b0 = e0 & 511, q0 = (e0 >> 9) & 0x3fffu;
+                        if (!(b0 >= 4 || (b0 == 3 && i - q0 <= 4096))) {
+                            if (av) tb_put(tb, i - 1);
+                            av = 1;
+                            i++;
+                            continue;
+                        }
+                        bool lazy = false;
+                        const uint32_t x = i + 1;
+                        if (b0 < 258 && x < npos) {
+                            if ((x >> 6) != hci) {
+                                hci = x >> 6;
+                                hcw = rfl64(HC[hci]);
+                            }
+                            if ((hcw >> (x & 63)) & 1) {
+                                const uint32_t e1 = group_get(g, x, npos, len);
+                                lazy = (e1 >> 31) || (e1 & 511) > b0;
+                            }
+                        }
+                        if (!lazy) {
+                            if (av) tb_put(tb, i - 1);
+                            tb_put(tb, ((i - q0) << 16) | (b0 - 3));
+                            i += b0;
+                            av = 0;
+                            continue;
+                        }
+                    }
+                }
+            }
+            const uint32_t pl = ml, pm = ms;
+            ml = 2;
+            if (i < npos && pl < 258) {
+                if ((i >> 6) != hci) {
+                    hci = i >> 6;
+                    hcw = rfl64(HC[hci]);
+                }
+                if ((hcw >> (i & 63)) & 1) {
+                    const uint32_t e = group_get(g, i, npos, len);
+                    uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
+                    if (e >> 31) {
+                        m = search(i, pl, len, m, q, &q);
+                        count(15);
+                    } else if (m <= pl) {
+                        m = 0;
+                    }
+                    if (m) {
+                        ml = m;
+                        ms = q;
+                        if (m == 3 && i - q > 4096) ml = 2; // TOO_FAR
+                    }
+                }
+            }
+            if (pl >= 3 && ml <= pl) {
+                tb_put(tb, ((i - 1 - pm) << 16) | (pl - 3));
+                i += pl - 1;
+                ml = 2;
+                av = 0;
+            } else {
+                if (av) tb_put(tb, i - 1);
+                av = 1;
+                i++;
+            }
+        }
+        if (av) tb_put(tb, i - 1);
+        tb_finish(tb);
+        wave_sync_global();
+        return rfl(tb.n);
     }
 
     // build_tree's heapify + merge loop (trees.c) on a register heap; returns the next
@@ -1104,9 +1352,7 @@ struct SmallWave {
         const uint32_t npos = len >= 3 ? len - 2 : 0;
         if (npos) {
             sort_positions(npos);
-            stamp(13);
             PMC_STOP(2, 0)
-            match_all(npos, len);
         }
         PMC_STOP(3, 0)
         stamp(1);
@@ -1114,7 +1360,7 @@ struct SmallWave {
         // (len - 3); literal = its position (dist 0), the byte is fetched in flush.
         uint32_t ntok;
         if (npos) {
-            ntok = parse(npos, len);
+            ntok = parse_ondemand(npos, len);
         } else { // no position with MIN_MATCH lookahead: all literals
             lit_run(0, 0, len);
             ntok = len;
@@ -1189,6 +1435,7 @@ __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
     w.H = w.R; // hash keys live in R until the ranks overwrite them
     w.cnt = to_lds<uint16_t>(base + L.cnt);
     w.M = to_lds<uint32_t>(base + L.M);
+    w.HC = to_lds<uint64_t>(base + L.M);
     w.ML = to_lds<uint64_t>(base + L.masks);
     w.MP = to_lds<uint64_t>(base + L.masks_p);
     w.tok = (PMC_GLB uint32_t *)(a.tokens + wave * kSlabSyms);

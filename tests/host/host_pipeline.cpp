@@ -227,7 +227,7 @@ int main(int argc, char **argv) {
     // v2 small-value path (pmc_deflate_small.hip match_all + search): every position's walk
     // over its first kPre chain candidates is done up front (best | q << 9 | cut << 31);
     // the parse resumes cut walks at candidate kPre.
-    const uint32_t kPre = 16;
+    const uint32_t kPre = 32; // = 64 / PMC_GROUP (pmc_deflate_small.hip)
     const bool pre = use_v2 && len <= 16382;
     std::vector<uint32_t> M(pre ? npos : 0);
     for (uint64_t i = 0; pre && i < npos; i++) {
@@ -385,75 +385,57 @@ int main(int argc, char **argv) {
     uint64_t match_start = 0, prev_match;
     bool avail = false;
     if (pre) {
-        // v2 segment walk (pmc_deflate_small.hip parse()): from a fresh state at p, literals
-        // [p, t) then the match at t; segments touching a cut walk run the exact step loop.
-        auto best_of = [&](uint64_t j) { return j < npos ? M[j] & 511 : 0u; };
-        auto is_cut = [&](uint64_t j) { return j < npos && (M[j] >> 31); };
-        auto usable = [&](uint64_t j) {
-            uint32_t bj = best_of(j), q = (M[j] >> 9) & 0x3fff;
-            return bj >= 4 || (bj == 3 && j - q <= 4096);
+        // v2 on-demand parse (pmc_deflate_small.hip parse_ondemand()): with no pending match,
+        // positions without chain candidates are skipped as literals; every other position
+        // steps deflate_slow exactly with longest_match = M (resumed by search_pre if cut).
+        auto has_cand = [&](uint64_t x) {
+            if (x >= npos || rank[x] == 0) return false;
+            uint64_t q = S[rank[x] - 1] & 0xffffffffull;
+            return q != 0 && (S[rank[x] - 1] >> 32) == (S[rank[x]] >> 32);
         };
-        auto stopL = [&](uint64_t j) { return j < npos && (usable(j) || is_cut(j)); };
-        auto stopP = [&](uint64_t j) {
-            bool impr = best_of(j) < 258 && j + 1 < npos && best_of(j + 1) > best_of(j);
-            return j < npos && (is_cut(j) || !impr);
-        };
-        uint64_t p = 0;
-        while (p < len) {
-            uint64_t j = p;
-            while (j < npos && !stopL(j)) j++;
-            if (j >= npos) {
-                for (uint64_t k = p; k < len; k++) emit(b[k]);
-                break;
-            }
-            if (!is_cut(j)) {
-                uint64_t t = j;
-                while (!stopP(t)) t++;
-                uint32_t bt = best_of(t);
-                bool ok = !is_cut(t);
-                if (ok && bt < 258 && t + 1 < npos) ok = !(is_cut(t + 1) && best_of(t + 1) <= bt);
-                if (ok) {
-                    for (uint64_t k = p; k < t; k++) emit(b[k]);
-                    emit((uint32_t)(t - ((M[t] >> 9) & 0x3fff)) << 16 | (bt - 3));
-                    p = t + bt;
-                    continue;
-                }
-            }
-            // positions [p, j) have no usable match: literals [p, j - 1), b[j - 1] pending
-            for (uint64_t k = p; k + 1 < j; k++) emit(b[k]);
-            uint64_t ii = j;
-            uint32_t ml = 2;
-            uint64_t ms = 0;
-            bool av = j > p, matched = false;
-            while (ii < len) {
-                uint32_t pl = ml;
-                uint64_t pm = ms;
-                ml = 2;
-                if (ii + 3 <= len && pl < 258) {
-                    uint64_t q = 0;
-                    uint32_t m = search_pre(ii, pl, &q);
-                    if (m) {
-                        ml = m;
-                        ms = q;
-                        if (m == 3 && ii - q > 4096) ml = 2;
-                    }
-                }
-                if (pl >= 3 && ml <= pl) {
-                    emit((uint32_t)(ii - 1 - pm) << 16 | (pl - 3));
-                    ii += pl - 1;
-                    matched = true;
-                    break;
-                } else if (av) {
-                    emit(b[ii - 1]);
-                    ii++;
-                } else {
+        uint64_t ii = 0;
+        uint32_t ml = 2;
+        uint64_t ms = 0;
+        bool av = false;
+        while (ii < len) {
+            if (ml == 2) {
+                uint64_t j = ii;
+                while (j < npos && !has_cand(j)) j++;
+                if (j >= npos) j = len;
+                if (j > ii) {
+                    uint64_t from = av ? ii - 1 : ii;
+                    for (uint64_t k = from; k + 1 < j; k++) emit(b[k]);
                     av = true;
-                    ii++;
+                    ii = j;
+                    if (ii >= len) break;
                 }
             }
-            if (!matched && av) emit(b[ii - 1]);
-            p = ii;
+            uint32_t pl = ml;
+            uint64_t pm = ms;
+            ml = 2;
+            if (ii < npos && pl < 258 && has_cand(ii)) {
+                uint64_t q = 0;
+                uint32_t m = search_pre(ii, pl, &q);
+                if (m) {
+                    ml = m;
+                    ms = q;
+                    if (m == 3 && ii - q > 4096) ml = 2;
+                }
+            }
+            if (pl >= 3 && ml <= pl) {
+                emit((uint32_t)(ii - 1 - pm) << 16 | (pl - 3));
+                ii += pl - 1;
+                ml = 2;
+                av = false;
+            } else if (av) {
+                emit(b[ii - 1]);
+                ii++;
+            } else {
+                av = true;
+                ii++;
+            }
         }
+        if (av) emit(b[ii - 1]);
         i = len;
         avail = false;
     }
