@@ -147,6 +147,7 @@ struct pmc_ctx {
     hipStream_t stream = nullptr;
     DevBuf tokens, dscratch;     // deflate symbol slabs / HBM working sets
     DevBuf fbscratch;            // per-wave Trees for the small kernel's serial fallback
+    DevBuf split;                // chunk arrays of the split small-value pipeline
     DevBuf staging;              // device side of host-API calls
     uint64_t *dbg = nullptr;     // diagnostic stamp sums (PMC_STAMPS builds)
     HostBuf pinned;              // host side of host-API calls
@@ -231,6 +232,14 @@ PMC_API int pmc_ctx_create(int device, pmc_ctx **out) {
                                 (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)deflate_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kLdsPerCu));
+    HIP_TRY(hipFuncSetAttribute((const void *)deflate_front_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kLdsPerCu));
+    HIP_TRY(hipFuncSetAttribute((const void *)deflate_back_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kLdsPerCu));
+    HIP_TRY(hipFuncSetAttribute((const void *)deflate_trees_kernel<kTreesCap>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu));
+    HIP_TRY(hipFuncSetAttribute((const void *)deflate_trees_kernel<kLCodes>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)inflate_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)inflate_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -253,6 +262,7 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     c->tokens.release();
     c->dscratch.release();
     c->fbscratch.release();
+    c->split.release();
     c->staging.release();
     c->pinned.release();
     (void)hipStreamDestroy(c->stream);
@@ -292,49 +302,112 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
     const uint64_t v1_lim = deflate_lds_limit();
     const uint64_t lds_cut = force_v1 ? std::min<uint64_t>(v1_lim, std::max<uint64_t>(max_len, 1))
                                       : std::min<uint64_t>(small_lim, std::max<uint64_t>(max_len, 1));
-    Launch Ls{};
-    uint64_t small_waves = 0, hbm_waves = 0, hbm_wb = 0;
-    const void *lds_kernel = force_v1 ? (const void *)deflate_kernel<false> : (const void *)deflate_small_kernel;
     uint64_t cap = (lds_cut + 63) & ~(uint64_t)63;
     cap = std::min<uint64_t>(cap, force_v1 ? v1_lim : small_lim);
-    const uint64_t lds_wb = force_v1 ? deflate_wave_bytes(false, cap) : deflate_small_wave_bytes(cap);
-    Ls = plan_lds(ctx, lds_kernel, lds_wb, n);
-    small_waves = (uint64_t)Ls.blocks * Ls.wpb;
+    uint64_t hbm_waves = 0, hbm_wb = 0;
     if (max_len > lds_cut) {
         hbm_wb = deflate_wave_bytes(true, max_len);
         hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 2,
                                                              (8ull << 30) / std::max<uint64_t>(hbm_wb, 1)));
         hbm_waves = std::min<uint64_t>(hbm_waves, n);
     }
-    // size every per-wave buffer before the first launch (no reallocation under a kernel)
-    int r = ctx->tokens.ensure(std::max(small_waves, hbm_waves) * kSlabSyms * sizeof(uint32_t));
-    if (r) return r;
-    r = ctx->fbscratch.ensure(small_waves * sizeof(Trees));
-    if (r) return r;
-    if (hbm_waves) {
-        r = ctx->dscratch.ensure(hbm_waves * hbm_wb);
+    // Small values: the split pipeline (pmc_deflate_split.hip: front -> lane-parallel trees ->
+    // back, chunk by chunk) unless PMC_DEFLATE_MONO=1 selects the single-kernel path.
+    static const bool mono = getenv("PMC_DEFLATE_MONO") && atoi(getenv("PMC_DEFLATE_MONO"));
+    if (!force_v1 && !mono) {
+        const uint64_t fwb = deflate_front_wave_bytes(cap), bwb = deflate_back_wave_bytes(cap);
+        Launch Lf = plan_lds(ctx, (const void *)deflate_front_kernel, fwb, n);
+        Launch Lb = plan_lds(ctx, (const void *)deflate_back_kernel, bwb, n);
+        static const uint64_t budget = (getenv("PMC_SPLIT_CHUNK_MB") ? (uint64_t)atoll(getenv("PMC_SPLIT_CHUNK_MB"))
+                                                                     : 4096ull) << 20;
+        const uint64_t per = split_value_bytes(cap);
+        uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(4096, budget / per));
+        chunk = (chunk + 63) & ~(uint64_t)63;
+        const uint64_t blocks = chunk / 64;
+        int r = ctx->split.ensure(chunk * cap * 4 + chunk * 4 + chunk * 4 + blocks * 64 * kSplitRows * 3 +
+                                  blocks * 64 * kMergeRows * 4 + (chunk + 1) * 4 + 1024);
         if (r) return r;
+        if (hbm_waves) {
+            r = ctx->tokens.ensure(hbm_waves * kSlabSyms * sizeof(uint32_t));
+            if (r) return r;
+            r = ctx->dscratch.ensure(hbm_waves * hbm_wb);
+            if (r) return r;
+        }
+        uint8_t *p = (uint8_t *)ctx->split.p;
+        a.cT = (uint32_t *)p;
+        p += chunk * cap * 4;
+        a.cN = (uint32_t *)p;
+        p += chunk * 4;
+        a.cP = (uint32_t *)p;
+        p += chunk * 4;
+        a.cG = (uint32_t *)p;
+        p += blocks * 64 * kMergeRows * 4;
+        a.cH = (uint16_t *)p;
+        p += blocks * 64 * kSplitRows * 2;
+        a.cL = (uint8_t *)p;
+        p += blocks * 64 * kSplitRows;
+        a.cD = (uint32_t *)p;
+        a.lds_max_len = lds_cut;
+        a.cap_len = cap;
+        const size_t tl_small = (size_t)(kTreesCap + 1) * 64 * 4 + 36 * 64 * 2;
+        const size_t tl_big = (size_t)(kLCodes + 1) * 64 * 4 + 36 * 64 * 2;
+        for (uint64_t first = 0; first < n; first += chunk) {
+            a.first = first;
+            a.count = std::min<uint64_t>(chunk, n - first);
+            const unsigned tb = (unsigned)((a.count + 63) / 64);
+            a.wave_bytes = fwb;
+            hipLaunchKernelGGL(deflate_front_kernel,
+                               dim3((unsigned)std::min<uint64_t>(Lf.blocks, (a.count + Lf.wpb - 1) / Lf.wpb)),
+                               dim3(64 * Lf.wpb), Lf.lds - kCrcTabBytes, st, a);
+            if (hipMemsetAsync(a.cD + a.count, 0, 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
+            hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap>, dim3(tb), dim3(64), tl_small, st, a);
+            hipLaunchKernelGGL(deflate_trees_kernel<kLCodes>, dim3(std::min<unsigned>(tb, (unsigned)ctx->cus)), dim3(64),
+                               tl_big, st, a);
+            a.wave_bytes = bwb;
+            hipLaunchKernelGGL(deflate_back_kernel,
+                               dim3((unsigned)std::min<uint64_t>(Lb.blocks, (a.count + Lb.wpb - 1) / Lb.wpb)),
+                               dim3(64 * Lb.wpb), Lb.lds, st, a);
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            set_err("deflate split pipeline", e);
+            return PMC_E_NO_DEVICE;
+        }
+    } else {
+        const void *lds_kernel = force_v1 ? (const void *)deflate_kernel<false> : (const void *)deflate_small_kernel;
+        const uint64_t lds_wb = force_v1 ? deflate_wave_bytes(false, cap) : deflate_small_wave_bytes(cap);
+        Launch Ls = plan_lds(ctx, lds_kernel, lds_wb, n);
+        const uint64_t small_waves = (uint64_t)Ls.blocks * Ls.wpb;
+        // size every per-wave buffer before the first launch (no reallocation under a kernel)
+        int r = ctx->tokens.ensure(std::max(small_waves, hbm_waves) * kSlabSyms * sizeof(uint32_t));
+        if (r) return r;
+        r = ctx->fbscratch.ensure(small_waves * sizeof(Trees));
+        if (r) return r;
+        if (hbm_waves) {
+            r = ctx->dscratch.ensure(hbm_waves * hbm_wb);
+            if (r) return r;
+        }
+        a.tokens = (uint32_t *)ctx->tokens.p;
+        a.lds_max_len = lds_cut;
+        a.cap_len = cap;
+        a.wave_bytes = lds_wb;
+        a.scratch = (uint8_t *)ctx->fbscratch.p;
+        if (force_v1) hipLaunchKernelGGL(deflate_kernel<false>, dim3(Ls.blocks), dim3(64 * Ls.wpb), Ls.lds, st, a);
+        else hipLaunchKernelGGL(deflate_small_kernel, dim3(Ls.blocks), dim3(64 * Ls.wpb), Ls.lds, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            set_err("deflate_kernel<lds>", e);
+            return PMC_E_NO_DEVICE;
+        }
     }
     a.tokens = (uint32_t *)ctx->tokens.p;
-    // ---- LDS kernel (values <= lds_cut) ----
-    a.lds_max_len = lds_cut;
-    a.cap_len = cap;
-    a.wave_bytes = lds_wb;
-    a.scratch = (uint8_t *)ctx->fbscratch.p;
-    if (force_v1) hipLaunchKernelGGL(deflate_kernel<false>, dim3(Ls.blocks), dim3(64 * Ls.wpb), Ls.lds, st, a);
-    else hipLaunchKernelGGL(deflate_small_kernel, dim3(Ls.blocks), dim3(64 * Ls.wpb), Ls.lds, st, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_err("deflate_kernel<lds>", e);
-        return PMC_E_NO_DEVICE;
-    }
     // ---- HBM kernel (values > lds_cut) ----
     if (hbm_waves) {
         a.cap_len = max_len;
         a.wave_bytes = hbm_wb;
         a.scratch = (uint8_t *)ctx->dscratch.p;
         hipLaunchKernelGGL(deflate_kernel<true>, dim3((unsigned)hbm_waves), dim3(64), kCrcTabBytes, st, a);
-        e = hipGetLastError();
+        hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
             set_err("deflate_kernel<hbm>", e);
             return PMC_E_NO_DEVICE;

@@ -2,6 +2,7 @@
 // One TU keeps the __constant__ tables in one module without relocatable device code.
 #include "pmc_deflate.hip"
 #include "pmc_deflate_small.hip"
+#include "pmc_deflate_split.hip"
 #include "pmc_inflate.hip"
 #include "pmc_misc.hip"
 #include "pmc_capi.hip"

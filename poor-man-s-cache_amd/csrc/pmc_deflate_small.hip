@@ -40,6 +40,7 @@ struct SmallLayout {
     uint64_t out_words;
     uint64_t T, cnt; // sort view
     uint64_t M, masks, masks_p; // parse view
+    uint64_t front_total, back_total; // split pipeline: front (stage..parse..histogram), back (emit)
 };
 
 __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
@@ -86,9 +87,13 @@ __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
     uint64_t t = f > s ? f : s;
     t = t > m ? t : m;
     L.total = a(t);
+    L.front_total = a(t);
+    L.back_total = a(f);
     return L;
 }
 uint64_t deflate_small_wave_bytes(uint64_t n) { return small_layout(n).total; }
+uint64_t deflate_front_wave_bytes(uint64_t n) { return small_layout(n).front_total; }
+uint64_t deflate_back_wave_bytes(uint64_t n) { return small_layout(n).back_total; }
 
 __device__ __forceinline__ uint32_t hash3(uint32_t w) {
     return ((w & 0xff) << 10 ^ ((w >> 8) & 0xff) << 5 ^ ((w >> 16) & 0xff)) & 0x7fffu;
@@ -1138,6 +1143,44 @@ struct SmallWave {
         return base - pos;
     }
 
+    // compress_block: every token's bits at its prefix-sum offset
+    __device__ uint64_t emit_symbols(uint32_t ntok, uint64_t bitpos) {
+        const int l = lane_id();
+        const Tables &TT = c_tables;
+        for (uint32_t t0 = 0; t0 < ntok; t0 += 64) {
+            const uint32_t t = t0 + (uint32_t)l;
+            uint32_t nb = 0;
+            uint64_t v = 0;
+            if (t < ntok) {
+                const uint32_t tk = tok[t], dist = tk >> 16, lc = dist ? tk & 0xff : b[tk & 0xffff];
+                if (dist == 0) {
+                    const uint32_t c = lcode[lc];
+                    v = c & 0xffff;
+                    nb = c >> 16;
+                } else {
+                    const uint32_t code = TT.length_code[lc];
+                    uint32_t c = lcode[code + kLiterals + 1];
+                    v = c & 0xffff;
+                    nb = c >> 16;
+                    const uint32_t xl = TT.extra_lbits[code];
+                    v |= (uint64_t)((lc - TT.base_length[code]) & ((1u << xl) - 1)) << nb;
+                    nb += xl;
+                    const uint32_t dm = dist - 1, dc = d_code(TT, dm);
+                    c = dcode[dc];
+                    v |= (uint64_t)(c & 0xffff) << nb;
+                    nb += c >> 16;
+                    const uint32_t xd = TT.extra_dbits[dc];
+                    v |= (uint64_t)((dm - TT.base_dist[dc]) & ((1u << xd) - 1)) << nb;
+                    nb += xd;
+                }
+            }
+            const uint32_t incl = wave_incl_scan(nb);
+            if (nb) or_bits_lds(bitpos + incl - nb, v, (int)nb);
+            bitpos += readlane(incl, 63);
+        }
+        return bitpos;
+    }
+
     // ---- block flush: trees, block type, emission (single final block) --------------------
     __device__ __noinline__ uint64_t flush(uint32_t ntok, uint32_t len, uint64_t bitpos) {
         const int l = lane_id();
@@ -1274,38 +1317,123 @@ struct SmallWave {
                 wave_sync();
             }
         }
-        // symbols
-        for (uint32_t t0 = 0; t0 < ntok; t0 += 64) {
-            const uint32_t t = t0 + (uint32_t)l;
-            uint32_t nb = 0;
-            uint64_t v = 0;
-            if (t < ntok) {
-                const uint32_t tk = tok[t], dist = tk >> 16, lc = dist ? tk & 0xff : b[tk & 0xffff];
-                if (dist == 0) {
-                    const uint32_t c = lcode[lc];
-                    v = c & 0xffff;
-                    nb = c >> 16;
-                } else {
-                    const uint32_t code = TT.length_code[lc];
-                    uint32_t c = lcode[code + kLiterals + 1];
-                    v = c & 0xffff;
-                    nb = c >> 16;
-                    const uint32_t xl = TT.extra_lbits[code];
-                    v |= (uint64_t)((lc - TT.base_length[code]) & ((1u << xl) - 1)) << nb;
-                    nb += xl;
-                    const uint32_t dm = dist - 1, dc = d_code(TT, dm);
-                    c = dcode[dc];
-                    v |= (uint64_t)(c & 0xffff) << nb;
-                    nb += c >> 16;
-                    const uint32_t xd = TT.extra_dbits[dc];
-                    v |= (uint64_t)((dm - TT.base_dist[dc]) & ((1u << xd) - 1)) << nb;
-                    nb += xd;
-                }
+        bitpos = emit_symbols(ntok, bitpos);
+        const uint32_t eob = lcode[kEndBlock];
+        wave_sync();
+        if (l == 0) or_bits_lds(bitpos, eob & 0xffff, (int)(eob >> 16));
+        bitpos += eob >> 16;
+        bitpos = (bitpos + 7) & ~(uint64_t)7;
+        wave_sync();
+        return bitpos;
+    }
+
+
+    // ---- split pipeline pieces (pmc_deflate_split.hip) ----------------------------------------
+    // histogram of the token slab into lfreq / dfreq (END_BLOCK counted once)
+    __device__ void histogram(uint32_t ntok) {
+        const int l = lane_id();
+        const Tables &TT = c_tables;
+        for (int s = l; s < 352; s += 64) lfreq[s] = 0;
+        wave_sync();
+        for (uint32_t t = l; t < ntok; t += 64) {
+            const uint32_t tk = tok[t], dist = tk >> 16, lc = dist ? tk & 0xff : b[tk & 0xffff];
+            if (dist == 0) {
+                lds_add(&lfreq[lc], 1u);
+            } else {
+                lds_add(&lfreq[TT.length_code[lc] + kLiterals + 1], 1u);
+                lds_add(&dfreq[d_code(TT, dist - 1)], 1u);
             }
-            const uint32_t incl = wave_incl_scan(nb);
-            if (nb) or_bits_lds(bitpos + incl - nb, v, (int)nb);
-            bitpos += readlane(incl, 63);
         }
+        if (l == 0) lfreq[kEndBlock] = 1;
+        wave_sync();
+    }
+    // gen_codes (trees.c) for code lengths Ls[0..elems): canonical code = next_code[len] +
+    // rank among equal lengths; code_out[s] = bit-reversed code | len << 16 (0: unused)
+    __device__ __noinline__ void codes_from_lengths(PMC_LDS const uint8_t *Ls, int elems, PMC_LDS uint32_t *code_out) {
+        const int l = lane_id();
+        uint32_t bl_count[16];
+#pragma unroll
+        for (int L = 0; L < 16; L++) bl_count[L] = 0;
+        for (int c0 = 0; c0 < elems; c0 += 64) {
+            const int s = c0 + l;
+            const uint32_t len = s < elems ? Ls[s] : 0u;
+#pragma unroll
+            for (int L = 1; L <= 15; L++) bl_count[L] += __builtin_popcountll(ballot(len == (uint32_t)L));
+        }
+        uint32_t next_code[16];
+        uint32_t code = 0;
+        next_code[0] = 0;
+#pragma unroll
+        for (int L = 1; L <= 15; L++) {
+            code = (code + (L > 1 ? bl_count[L - 1] : 0u)) << 1;
+            next_code[L] = code;
+        }
+        for (int c0 = 0; c0 < elems; c0 += 64) {
+            const int s = c0 + l;
+            const uint32_t len = s < elems ? Ls[s] : 0u;
+            uint32_t mycode = 0;
+#pragma unroll
+            for (int L = 1; L <= 15; L++) {
+                const uint64_t mk = ballot(len == (uint32_t)L);
+                if (len == (uint32_t)L) mycode = next_code[L] + popc_lt(mk);
+                next_code[L] += __builtin_popcountll(mk);
+            }
+            if (s < elems) code_out[s] = len ? ((__builtin_bitreverse32(mycode) >> (32 - len)) | (len << 16)) : 0u;
+        }
+        wave_sync();
+    }
+    // the block as planned by deflate_trees_kernel: plan = type | l_max << 2 | d_max << 11 |
+    // max_blindex << 16 (type 0 stored, 1 fixed, 2 dynamic); Ls = lit/len, dist, bl lengths
+    __device__ uint64_t emit_planned(uint32_t ntok, uint32_t len, uint64_t bitpos, uint32_t plan,
+                                     PMC_LDS const uint8_t *Ls) {
+        const int l = lane_id();
+        const Tables &TT = c_tables;
+        const uint32_t type = plan & 3;
+        if (type == 0) {
+            if (l == 0) or_bits_lds(bitpos, 1u, 3);
+            bitpos = (bitpos + 3 + 7) & ~(uint64_t)7;
+            const uint64_t o = bitpos >> 3;
+            wave_sync();
+            if (l < 4) {
+                uint32_t v = l < 2 ? len : ~len;
+                outb[o + l] = (uint8_t)(v >> (8 * (l & 1)));
+            }
+            for (uint32_t k = l; k < len; k += 64) outb[o + 4 + k] = b[k];
+            bitpos += (4 + (uint64_t)len) * 8;
+            wave_sync();
+            return bitpos;
+        }
+        if (type == 1) {
+            for (int s = l; s < 288; s += 64)
+                lcode[s] = s < kLCodes ? (uint32_t)TT.static_ltree[s].fc | ((uint32_t)TT.static_ltree[s].dl << 16) : 0u;
+            if (l < 32) dcode[l] = l < kDCodes ? (uint32_t)TT.static_dtree[l].fc | ((uint32_t)TT.static_dtree[l].dl << 16) : 0u;
+            if (l == 0) or_bits_lds(bitpos, (1u << 1) | 1u, 3);
+            bitpos += 3;
+            wave_sync();
+        } else {
+            const int l_max = (int)((plan >> 2) & 511), d_max = (int)((plan >> 11) & 31), mbi = (int)((plan >> 16) & 31);
+            codes_from_lengths(Ls, kLCodes, lcode);
+            codes_from_lengths(Ls + kLCodes, kDCodes, dcode);
+            codes_from_lengths(Ls + kLCodes + kDCodes, kBLCodes, blcode);
+            PMC_LDS uint16_t *runL = runs, *runD = runs + 288;
+            scan_runs(lcode, l_max, runL);
+            scan_runs(dcode, d_max, runD);
+            wave_sync();
+            const int lcodes = l_max + 1, dcodes = d_max + 1, blcodes = mbi + 1;
+            if (l == 0) {
+                or_bits_lds(bitpos, (2u << 1) | 1u, 3);
+                or_bits_lds(bitpos + 3, (uint32_t)(lcodes - 257), 5);
+                or_bits_lds(bitpos + 8, (uint32_t)(dcodes - 1), 5);
+                or_bits_lds(bitpos + 13, (uint32_t)(blcodes - 4), 4);
+            }
+            if (l < blcodes) or_bits_lds(bitpos + 17 + 3 * l, blcode[TT.bl_order[l]] >> 16, 3);
+            bitpos += 17 + 3 * (uint64_t)blcodes;
+            wave_sync();
+            bitpos += send_runs(lcode, lcodes - 1, runL, bitpos);
+            bitpos += send_runs(dcode, dcodes - 1, runD, bitpos);
+            wave_sync();
+        }
+        bitpos = emit_symbols(ntok, bitpos);
         const uint32_t eob = lcode[kEndBlock];
         wave_sync();
         if (l == 0) or_bits_lds(bitpos, eob & 0xffff, (int)(eob >> 16));
@@ -1329,6 +1457,79 @@ struct SmallWave {
             pos += (uint64_t)n;
         }
     };
+
+    // ---- split pipeline: front half (stage, hash sort, lazy parse, histograms) ------------
+    __device__ void stage(const uint8_t *src, uint32_t len) {
+        const int l = lane_id();
+        const uint32_t padded = (len + 32) & ~3u;
+        if ((((uintptr_t)src) & 3) == 0) {
+            const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src);
+            const uint32_t full = len >> 2;
+            for (uint32_t k = l; k < padded / 4; k += 64) bw[k] = k < full ? s4[k] : 0u;
+            wave_sync();
+            if ((uint32_t)l < (len & 3)) b[full * 4 + l] = src[full * 4 + l];
+        } else {
+            for (uint32_t k = l; k < padded / 4; k += 64) bw[k] = 0;
+            wave_sync();
+            for (uint32_t k = l; k < len; k += 64) b[k] = src[k];
+        }
+        wave_sync();
+    }
+    __device__ uint32_t run_front(const uint8_t *src, uint32_t len) {
+        stage(src, len);
+        stamp(0);
+        const uint32_t npos = len >= 3 ? len - 2 : 0;
+        uint32_t ntok;
+        if (npos) {
+            sort_positions(npos);
+            stamp(1);
+            ntok = parse_ondemand(npos, len);
+        } else {
+            lit_run(0, 0, len);
+            ntok = len;
+        }
+        wave_sync_global();
+        stamp(2);
+        histogram(ntok);
+        stamp(6);
+        return ntok;
+    }
+    // ---- split pipeline: back half (CRC, codes from the planned lengths, emission) -------
+    __device__ int run_back(const uint8_t *src, uint32_t len, uint32_t ntok, uint32_t plan, PMC_LDS const uint8_t *Ls,
+                            uint8_t *dst, uint32_t dst_cap, uint32_t *dst_len) {
+        const int l = lane_id();
+        stage(src, len);
+        const uint32_t crc = wave_crc32(b, len, crc_tab);
+        for (uint64_t k = l; k < out_words; k += 64) outw[k] = 0;
+        wave_sync();
+        if (l < 10) {
+            const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 2, 3};
+            outb[l] = hdr[l];
+        }
+        wave_sync();
+        stamp(0);
+        uint64_t bitpos = emit_planned(ntok, len, 80, plan, Ls);
+        stamp(4);
+        uint64_t nbytes = bitpos >> 3;
+        if (l < 8) {
+            uint32_t v = l < 4 ? crc : len;
+            outb[nbytes + l] = (uint8_t)(v >> (8 * (l & 3)));
+        }
+        nbytes += 8;
+        wave_sync();
+        if (nbytes > dst_cap) return PMC_E_CAPACITY_DEV;
+        if ((((uintptr_t)dst) & 3) == 0) {
+            uint32_t *d4 = reinterpret_cast<uint32_t *>(dst);
+            const uint64_t full = nbytes >> 2;
+            for (uint64_t k = l; k < full; k += 64) d4[k] = outw[k];
+            if ((uint64_t)l < (nbytes & 3)) dst[full * 4 + l] = outb[full * 4 + l];
+        } else {
+            for (uint64_t k = l; k < nbytes; k += 64) dst[k] = outb[k];
+        }
+        if (l == 0) *dst_len = (uint32_t)nbytes;
+        stamp(5);
+        return 0;
+    }
 
     // ---- one value ----------------------------------------------------------------------
     __device__ int run(const uint8_t *src, uint32_t len, uint8_t *dst, uint32_t dst_cap, uint32_t *dst_len) {
@@ -1403,6 +1604,44 @@ struct SmallWave {
         return 0;
     }
 };
+
+__device__ inline void small_wave_init(SmallWave &w, uint8_t *base, const SmallLayout &L, const DeflateArgs &a,
+                                       uint32_t *crc_tab) {
+    w.b = to_lds<uint8_t>(base + L.bytes);
+    w.bw = to_lds<uint32_t>(base + L.bytes);
+    w.S = to_lds<uint16_t>(base + L.S);
+    w.R = to_lds<uint16_t>(base + L.R);
+    w.lfreq = to_lds<uint32_t>(base + L.freq);
+    w.dfreq = w.lfreq + 288;
+    w.blfreq = w.dfreq + 32;
+    w.outw = to_lds<uint32_t>(base + L.out);
+    w.outb = to_lds<uint8_t>(base + L.out);
+    w.out_words = (uint32_t)L.out_words;
+    w.lcode = to_lds<uint32_t>(base + L.lcode);
+    w.dcode = to_lds<uint32_t>(base + L.dcode);
+    w.blcode = to_lds<uint32_t>(base + L.blcode);
+    w.dad = to_lds<uint16_t>(base + L.dad);
+    w.dep = to_lds<uint8_t>(base + L.dep);
+    w.runs = to_lds<uint16_t>(base + L.runs);
+    w.T = to_lds<uint16_t>(base + L.T);
+    w.H = w.R; // hash keys live in R until the ranks overwrite them
+    w.cnt = to_lds<uint16_t>(base + L.cnt);
+    w.M = to_lds<uint32_t>(base + L.M);
+    w.HC = to_lds<uint64_t>(base + L.M);
+    w.crc_tab = to_lds<const uint32_t>((void *)crc_tab);
+    for (int k = 0; k < 16; k++) w.st[k] = 0;
+    w.stop = a.stop_after;
+#ifdef PMC_STAMPS
+    w.t_last = __builtin_amdgcn_s_memtime();
+#endif
+}
+
+__device__ inline void small_wave_stamps_out(const SmallWave &w, const DeflateArgs &a) {
+#ifdef PMC_STAMPS
+    if (lane_id() == 0 && a.dbg)
+        for (int k = 0; k < 16; k++) atomicAdd((unsigned long long *)&a.dbg[k], (unsigned long long)w.st[k]);
+#endif
+}
 
 __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];

@@ -1,0 +1,345 @@
+// pmc_deflate_split.hip -- the small-value compressor as three kernels per chunk of values:
+//
+//   deflate_front_kernel  one wave per value: stage, hash sort, lazy parse (deflate_slow with
+//                         on-demand longest_match), symbol histograms -> tokens + histograms
+//   deflate_trees_kernel  one LANE per value: zlib trees.c build_tree / gen_bitlen (exact
+//                         binary heap, overflow fix-up), scan_tree, build_bl_tree and the
+//                         stored/fixed/dynamic choice -> code lengths + block plan
+//   deflate_back_kernel   one wave per value: CRC-32, canonical codes, tree headers,
+//                         compress_block emission, gzip framing -> output member
+//
+// Why the middle kernel is lane-parallel: Huffman construction is a long chain of dependent
+// heap operations on ~50-300 entries.  Run by a whole wave it is scalar-unit work (the CU's
+// one scalar unit is the bottleneck of the wave-per-value kernel); run by one lane it costs
+// 1/64 of the issue slots per value and its heap sits in conflict-free LDS columns
+// (entry i of lane l at word i * 64 + l).
+//
+// Output bytes equal deflate_small_kernel's, i.e. zlib 1.2.11 level 9
+// (reference: /root/reference/src/compressor/gzip_compressor.cpp:3-50).
+#include <hip/hip_runtime.h>
+
+#include "pmc_device.hpp"
+#include "pmc_kernels.hpp"
+
+namespace pmc {
+
+// chunk arrays: value v of a chunk is column v & 63 of block v >> 6
+__device__ __forceinline__ uint64_t col_index(uint64_t v, uint32_t row) {
+    return ((v >> 6) * kSplitRows + row) * 64 + (v & 63);
+}
+
+// ---- front -------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256, 4) deflate_front_kernel(DeflateArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + wib;
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    uint8_t *base = lds + (uint64_t)wib * a.wave_bytes;
+    const SmallLayout L = small_layout(a.cap_len);
+    SmallWave w;
+    small_wave_init(w, base, L, a, nullptr);
+    for (uint64_t g = wave * 64; g < a.count; g += nwaves * 64) {
+        const uint64_t vl = g + (uint64_t)l;
+        const uint32_t myl = vl < a.count ? a.src_len[a.first + vl] : 0u;
+        uint64_t todo = ballot(vl < a.count && myl != 0 && myl <= a.lds_max_len);
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint64_t v = g + (uint64_t)j, gv = a.first + v;
+            const uint32_t len = readlane(myl, j);
+            w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
+            const uint32_t ntok = w.run_front(a.src + a.src_off[gv], len);
+            // histograms -> column v of the chunk's interleaved u16 table
+            for (int s = l; s < kLCodes + kDCodes; s += 64)
+                a.cH[col_index(v, (uint32_t)s)] = (uint16_t)(s < kLCodes ? w.lfreq[s] : w.dfreq[s - kLCodes]);
+            if (l == 0) a.cN[v] = ntok;
+        }
+    }
+    small_wave_stamps_out(w, a);
+}
+
+// ---- trees (one lane per value) ------------------------------------------------------------------
+// Packed heap entry, as in the wave kernel: (freq << 5 | depth) << 10 | node, so zlib's
+// smaller(n, m) (freq, then depth, <=) is key(n) <= key(m) with key = entry >> 10.
+template <int CAP>
+struct LaneTrees {
+    PMC_LDS uint32_t *hp;  // heap, entry i at hp[i * 64]  (column of this lane)
+    PMC_LDS uint16_t *blc; // bl_count[16]
+    PMC_LDS uint16_t *blf; // bit-length tree frequencies [19]
+    const uint16_t *hist;  // global column: hist[sym * 64]
+    uint8_t *lens;         // global column: lens[sym * 64]
+    uint32_t *mg;          // global column: merge list, mg[i * 64]
+    bool deferred = false;
+
+    __device__ uint32_t H(uint32_t i) const { return hp[i * 64]; }
+    __device__ void setH(uint32_t i, uint32_t v) { hp[i * 64] = v; }
+
+    // pqdownheap (trees.c)
+    __device__ void down(uint32_t k, uint32_t n) {
+        const uint32_t v = H(k), kv = v >> 10;
+        uint32_t j = k << 1;
+        while (j <= n) {
+            uint32_t x = H(j);
+            if (j < n) {
+                const uint32_t y = H(j + 1);
+                if ((y >> 10) <= (x >> 10)) {
+                    j++;
+                    x = y;
+                }
+            }
+            if (kv <= (x >> 10)) break;
+            setH(k, x);
+            k = j;
+            j <<= 1;
+        }
+        setH(k, v);
+    }
+
+    // build_tree + gen_bitlen (trees.c) for one tree whose frequencies are freq(s), s < elems;
+    // leaf lengths go to lens[(row0 + s) * 64].  Returns max_code (-1 and `deferred` when the
+    // heap would exceed CAP entries).
+    template <class Freq>
+    __device__ int build(Freq freq, int elems, uint32_t row0, const CtData *stree, const uint8_t *extra, int extra_base,
+                         int max_length, int64_t &opt, int64_t &stat) {
+        int heap_len = 0, max_code = -1;
+        // (frequencies fetched 8 at a time so the loads overlap)
+        for (int n0 = 0; n0 < elems; n0 += 8) {
+            uint32_t f8[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) f8[k] = n0 + k < elems ? freq(n0 + k) : 0u;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if (f8[k]) {
+                    if (heap_len == CAP) {
+                        deferred = true;
+                        return -1;
+                    }
+                    setH(++heap_len, f8[k] << 15 | (uint32_t)(n0 + k));
+                    max_code = n0 + k;
+                }
+            }
+        }
+        while (heap_len < 2) { // at least two codes (dummy leaves of frequency 1)
+            const int node = max_code < 2 ? ++max_code : 0;
+            setH(++heap_len, 1u << 15 | (uint32_t)node);
+            opt--;
+            if (stree) stat -= stree[node].dl;
+        }
+        for (int n = heap_len / 2; n >= 1; n--) down((uint32_t)n, (uint32_t)heap_len);
+        uint32_t node = (uint32_t)elems, nm = 0;
+        do {
+            const uint32_t n = H(1);
+            setH(1, H((uint32_t)heap_len));
+            heap_len--;
+            down(1, (uint32_t)heap_len);
+            const uint32_t m = H(1);
+            mg[(2 * nm) * 64] = n;
+            mg[(2 * nm + 1) * 64] = m;
+            nm++;
+            const uint32_t kn = n >> 10, km = m >> 10, dn = kn & 31, dm = km & 31;
+            const uint32_t d = (dn >= dm ? dn : dm) + 1;
+            setH(1, ((((kn >> 5) + (km >> 5)) << 5) | d) << 10 | node);
+            node++;
+            down(1, (uint32_t)heap_len);
+        } while (heap_len >= 2);
+        // gen_bitlen: merges in reverse (zlib's heap[heap_max..] order: m before n); the
+        // lengths of internal nodes reuse the heap's column (node elems + i - 1 at slot i)
+        const uint32_t K = nm;
+        uint32_t overflow = 0;
+        for (int b = 0; b <= kMaxBits; b++) blc[b * 64] = 0;
+        setH(K, 0);
+        for (uint32_t i = K; i >= 1; i--) {
+            const uint32_t L = H(i);
+#pragma unroll
+            for (int c = 1; c >= 0; c--) {
+                const uint32_t key = mg[(2 * (i - 1) + c) * 64], x = key & 1023;
+                uint32_t bits = L + 1;
+                if (bits > (uint32_t)max_length) {
+                    bits = (uint32_t)max_length;
+                    overflow++;
+                }
+                if (x >= (uint32_t)elems) {
+                    setH(x - (uint32_t)elems + 1, bits);
+                } else {
+                    lens[(row0 + x) * 64] = (uint8_t)bits;
+                    blc[bits * 64]++;
+                    const uint32_t f = key >> 15;
+                    const uint32_t xb = (int)x >= extra_base ? extra[x - extra_base] : 0u;
+                    opt += (int64_t)f * (bits + xb);
+                    if (stree) stat += (int64_t)f * (stree[x].dl + xb);
+                }
+            }
+        }
+        if (overflow) {
+            int ov = (int)overflow;
+            do {
+                int bits = max_length - 1;
+                while (blc[bits * 64] == 0) bits--;
+                blc[bits * 64]--;
+                blc[(bits + 1) * 64] += 2;
+                blc[max_length * 64]--;
+                ov -= 2;
+            } while (ov > 0);
+            // leaves in zlib's heap[--h] order from the top: n_1, m_1, n_2, m_2, ...
+            uint32_t idx = 0;
+            for (int bits = max_length; bits != 0; bits--) {
+                uint32_t n = blc[bits * 64];
+                while (n != 0) {
+                    const uint32_t key = mg[idx * 64], x = key & 1023;
+                    idx++;
+                    if (x >= (uint32_t)elems) continue;
+                    const uint32_t cur = lens[(row0 + x) * 64];
+                    if (cur != (uint32_t)bits) {
+                        opt += ((int64_t)bits - (int64_t)cur) * (int64_t)(key >> 15);
+                        lens[(row0 + x) * 64] = (uint8_t)bits;
+                    }
+                    n--;
+                }
+            }
+        }
+        return max_code;
+    }
+
+    // scan_tree (trees.c): bit-length tree frequencies for lengths lens[row0 .. row0 + max_code]
+    __device__ void scan(uint32_t row0, int max_code) {
+        int prevlen = -1, nextlen = lens[row0 * 64], count = 0, max_count = 7, min_count = 4;
+        if (nextlen == 0) max_count = 138, min_count = 3;
+        int w0 = -8;
+        uint64_t pk = 0; // lengths w0 .. w0 + 7, one byte each (fetched 8 at a time so the loads overlap)
+        for (int n = 0; n <= max_code; n++) {
+            const int curlen = nextlen, nx = n + 1;
+            if (nx <= max_code) {
+                if (nx >= w0 + 8) {
+                    w0 = nx & ~7;
+                    pk = 0;
+#pragma unroll
+                    for (int k = 0; k < 8; k++)
+                        pk |= (uint64_t)(w0 + k <= max_code ? lens[(row0 + w0 + k) * 64] : 0u) << (8 * k);
+                }
+                nextlen = (int)((pk >> (8 * (nx - w0))) & 0xff);
+            } else {
+                nextlen = 0xffff;
+            }
+            if (++count < max_count && curlen == nextlen) continue;
+            if (count < min_count) {
+                blf[curlen * 64] += count;
+            } else if (curlen != 0) {
+                if (curlen != prevlen) blf[curlen * 64]++;
+                blf[kRep3_6 * 64]++;
+            } else if (count <= 10) {
+                blf[kRepz3_10 * 64]++;
+            } else {
+                blf[kRepz11_138 * 64]++;
+            }
+            count = 0;
+            prevlen = curlen;
+            if (nextlen == 0) max_count = 138, min_count = 3;
+            else if (curlen == nextlen) max_count = 6, min_count = 3;
+            else max_count = 7, min_count = 4;
+        }
+    }
+};
+
+template <int CAP>
+__device__ void trees_value(const DeflateArgs &a, uint64_t v, PMC_LDS uint32_t *col, PMC_LDS uint16_t *aux) {
+    const uint32_t len = a.src_len[a.first + v];
+    if (len == 0 || len > a.lds_max_len) return;
+    const Tables &TT = c_tables;
+    LaneTrees<CAP> t;
+    t.hp = col;
+    t.blc = aux;
+    t.blf = aux + 16 * 64;
+    t.hist = a.cH + col_index(v, 0);
+    t.lens = a.cL + col_index(v, 0);
+    t.mg = a.cG + ((v >> 6) * kMergeRows) * 64 + (v & 63);
+    for (uint32_t s = 0; s < kSplitRows; s++) t.lens[s * 64] = 0;
+    int64_t opt = 0, stat = 0;
+    auto hist = [&](int s) -> uint32_t { return t.hist[s * 64]; };
+    const int l_max = t.build(hist, kLCodes, 0, TT.static_ltree, TT.extra_lbits, kLiterals + 1, kMaxBits, opt, stat);
+    if (t.deferred) {
+        a.cP[v] = kPlanDeferred;
+        a.cD[atomicAdd(a.cD + a.count, 1u)] = (uint32_t)v;
+        return;
+    }
+    auto dhist = [&](int s) -> uint32_t { return t.hist[(kLCodes + s) * 64]; };
+    const int d_max = t.build(dhist, kDCodes, kLCodes, TT.static_dtree, TT.extra_dbits, 0, kMaxBits, opt, stat);
+    for (int s = 0; s < kBLCodes; s++) t.blf[s * 64] = 0;
+    t.scan(0, l_max);
+    t.scan(kLCodes, d_max);
+    auto bfreq = [&](int s) -> uint32_t { return t.blf[s * 64]; };
+    t.build(bfreq, kBLCodes, kLCodes + kDCodes, nullptr, TT.extra_blbits, 0, kMaxBLBits, opt, stat);
+    int mbi;
+    for (mbi = kBLCodes - 1; mbi >= 3; mbi--)
+        if (t.lens[(kLCodes + kDCodes + TT.bl_order[mbi]) * 64] != 0) break;
+    opt += 3 * ((int64_t)mbi + 1) + 5 + 5 + 4;
+    uint32_t opt_lenb = (uint32_t)(((uint64_t)opt + 3 + 7) >> 3);
+    const uint32_t static_lenb = (uint32_t)(((uint64_t)stat + 3 + 7) >> 3);
+    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+    const uint32_t type = len + 4 <= opt_lenb ? 0u : static_lenb == opt_lenb ? 1u : 2u;
+    a.cP[v] = type | (uint32_t)l_max << 2 | (uint32_t)d_max << 11 | (uint32_t)mbi << 16;
+}
+
+// Values whose literal/length tree needs more than CAP heap entries are listed in cD (count at
+// cD[count]) and planned by the CAP = kLCodes instance, a small grid that walks that list.
+template <int CAP>
+__global__ void __launch_bounds__(64) deflate_trees_kernel(DeflateArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t tl[];
+    const uint32_t l = threadIdx.x;
+    PMC_LDS uint32_t *col = to_lds<uint32_t>(tl + l);
+    PMC_LDS uint16_t *aux = to_lds<uint16_t>((uint16_t *)(tl + (CAP + 1) * 64) + l);
+    if (CAP != kLCodes) {
+        const uint64_t v = (uint64_t)blockIdx.x * 64 + l;
+        if (v < a.count) trees_value<CAP>(a, v, col, aux);
+    } else {
+        const uint32_t nd = a.cD[a.count];
+        for (uint32_t k = blockIdx.x * 64 + l; k < nd; k += gridDim.x * 64) trees_value<CAP>(a, a.cD[k], col, aux);
+    }
+}
+template __global__ void deflate_trees_kernel<kTreesCap>(DeflateArgs);
+template __global__ void deflate_trees_kernel<kLCodes>(DeflateArgs);
+
+// ---- back --------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256, 4) deflate_back_kernel(DeflateArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
+    __syncthreads();
+    const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + wib;
+    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
+    uint8_t *base = lds + 1024 + (uint64_t)wib * a.wave_bytes;
+    const SmallLayout L = small_layout(a.cap_len);
+    SmallWave w;
+    small_wave_init(w, base, L, a, crc_tab);
+    PMC_LDS uint8_t *Ls = to_lds<uint8_t>(base + L.dad); // code lengths (dad/dep are unused here)
+    for (uint64_t g = wave * 64; g < a.count; g += nwaves * 64) {
+        const uint64_t vl = g + (uint64_t)l;
+        const uint32_t myl = vl < a.count ? a.src_len[a.first + vl] : 0u;
+        uint64_t todo = ballot(vl < a.count && myl <= a.lds_max_len);
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint64_t v = g + (uint64_t)j, gv = a.first + v;
+            const uint32_t len = readlane(myl, j);
+            if (len == 0) {
+                if (l == 0) {
+                    a.rc[gv] = PMC_INVALID_INPUT_DEV;
+                    a.dst_len[gv] = 0;
+                }
+                continue;
+            }
+            const uint32_t ntok = a.cN[v], plan = a.cP[v];
+            for (uint32_t s = l; s < kSplitRows; s += 64) Ls[s] = a.cL[col_index(v, s)];
+            w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
+            const int rc = w.run_back(a.src + a.src_off[gv], len, ntok, plan, Ls, a.dst + a.dst_off[gv],
+                                      a.dst_cap[gv], a.dst_len + gv);
+            if (l == 0) {
+                a.rc[gv] = rc;
+                if (rc) a.dst_len[gv] = 0;
+            }
+        }
+    }
+    small_wave_stamps_out(w, a);
+}
+
+} // namespace pmc

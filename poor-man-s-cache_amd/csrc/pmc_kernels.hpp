@@ -36,7 +36,28 @@ struct DeflateArgs {
     uint8_t *scratch;     // per-wave HBM working sets (HBM variant)
     uint64_t *dbg;        // PMC_STAMPS builds: per-phase cycle sums (else unused)
     int32_t stop_after;   // PMC_STAMPS builds: end each value after phase k (cost attribution)
+    // split small-value pipeline (pmc_deflate_split.hip), one chunk of values at a time:
+    // value first + v (v < count) owns slot v of the per-value arrays and column v & 63 of
+    // block v >> 6 of the interleaved ones
+    uint64_t first, count;
+    uint32_t *cT;  // LZ77 tokens, stride cap_len
+    uint32_t *cN;  // token count per value
+    uint16_t *cH;  // symbol histograms, interleaved [block][kSplitRows][64]
+    uint8_t *cL;   // code lengths lit/len | dist | bit-length, interleaved [block][kSplitRows][64]
+    uint32_t *cP;  // block plan per value
+    uint32_t *cG;  // trees kernel merge lists, interleaved [block][kMergeRows][64]
+    uint32_t *cD;  // values deferred to the large-heap trees pass; their number at cD[count]
 };
+
+constexpr uint32_t kSplitRows = 336;  // 286 lit/len + 30 dist + 19 bit-length (+1)
+constexpr uint32_t kMergeRows = 572;  // 2 heap entries per merge, <= 285 merges
+constexpr uint32_t kPlanDeferred = 0xffffffffu;
+constexpr int kTreesCap = 96;         // lane heap capacity of the first trees pass
+
+// bytes of chunk scratch per value of the split pipeline
+__host__ __device__ inline uint64_t split_value_bytes(uint64_t cap) {
+    return cap * 4 + 4 + kSplitRows * 2 + kSplitRows + 4 + kMergeRows * 4 + 4;
+}
 
 struct InflateArgs {
     const uint8_t *src;
@@ -62,6 +83,12 @@ uint64_t inflate_wave_bytes(bool hbm, uint64_t max_out, uint64_t max_in);
 template <bool kHbm>
 __global__ void deflate_kernel(DeflateArgs a);
 __global__ void deflate_small_kernel(DeflateArgs a);
+uint64_t deflate_front_wave_bytes(uint64_t n);
+uint64_t deflate_back_wave_bytes(uint64_t n);
+__global__ void deflate_front_kernel(DeflateArgs a);
+template <int CAP>
+__global__ void deflate_trees_kernel(DeflateArgs a);
+__global__ void deflate_back_kernel(DeflateArgs a);
 template <bool kHbm>
 __global__ void inflate_kernel(InflateArgs a);
 

@@ -165,6 +165,33 @@ def test_ragged_edge_sizes_vs_oracle(ctx, D, golden):
         assert back[j] == vals[k]
 
 
+def test_skewed_histograms_vs_oracle(ctx, D):
+    """Fibonacci-weighted symbol streams: deep Huffman trees (zlib's gen_bitlen length-limit
+    fix-up for the 15-bit and 7-bit trees), wide alphabets (the trees pass's large-heap
+    path) and everything between, byte-exact against the oracle."""
+    from oracle import pyoracle as O
+    rng = np.random.default_rng(11)
+    fib = [1, 1]
+    while len(fib) < 40:
+        fib.append(fib[-1] + fib[-2])
+    vals = []
+    for size in (200, 1000, 3000, 9000, 16000):
+        for nsym in (8, 20, 40, 120, 255):
+            w = np.array([fib[min(i, len(fib) - 1)] for i in range(nsym)][::-1], dtype=np.float64)
+            w = w / w.sum()
+            syms = rng.permutation(np.arange(1, 256))[:nsym].astype(np.uint8)
+            vals.append(bytes(rng.choice(syms, size=size, p=w)))
+        vals.append(bytes(rng.integers(1, 256, size, dtype=np.uint8)))
+    b = D.pack(vals)
+    out, rc = D.compress(ctx, b)
+    sync()
+    rc = rc.cpu().numpy()
+    got = out.host_items()
+    for k, v in enumerate(vals):
+        assert rc[k] == 0, (k, len(v), rc[k])
+        assert got[k] == O.compress(v), (k, len(v))
+
+
 @pytest.mark.parametrize("vlen,kind,n", [(256, 0, 200_000), (1024, 0, 200_000), (4096, 0, 40_000),
                                          (1024, 1, 50_000)])
 def test_roundtrip_at_scale(ctx, D, golden, vlen, kind, n):
