@@ -92,7 +92,25 @@ __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
     return L;
 }
 uint64_t deflate_small_wave_bytes(uint64_t n) { return small_layout(n).total; }
-uint64_t deflate_front_wave_bytes(uint64_t n) { return small_layout(n).front_total; }
+// split-pipeline front: bytes | S | R | X (sort table, then the parse's HC bits); the symbol
+// histograms overlay S and R after the parse
+struct FrontLayout {
+    uint64_t bytes, S, R, X, freq, total;
+};
+__host__ __device__ inline FrontLayout front_layout(uint64_t n) {
+    auto a = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
+    FrontLayout F;
+    F.bytes = 0;
+    F.S = a(n + 32);
+    F.R = F.S + a(2 * n + 2);
+    F.X = F.R + a(2 * n + 2);
+    const uint64_t xs = a(((n + 63) / 64) * 8) > 1024 ? a(((n + 63) / 64) * 8) : 1024;
+    F.freq = F.S;
+    const uint64_t t1 = F.X + xs, t2 = F.freq + 352 * 4;
+    F.total = a(t1 > t2 ? t1 : t2);
+    return F;
+}
+uint64_t deflate_front_wave_bytes(uint64_t n) { return front_layout(n).total; }
 uint64_t deflate_back_wave_bytes(uint64_t n) { return small_layout(n).back_total; }
 
 __device__ __forceinline__ uint32_t hash3(uint32_t w) {
@@ -319,6 +337,68 @@ struct SmallWave {
                     cnt[slot] = (uint16_t)(at + 1);
                     dst[at] = (uint16_t)p;
                 }
+            }
+            wave_sync();
+        }
+        for (uint32_t k = l; k < npos; k += 64) R[S[k]] = (uint16_t)k;
+        wave_sync();
+    }
+
+    // ---- stable 2-pass LSD radix sort of positions by hash (8 + 7 bits) --------------------
+    // Keys are recomputed from the bytes in every phase (no key array), T aliases R (ranks are
+    // written last) and the only scratch is a 256-counter table, so the sort needs no LDS
+    // beyond S, R and 1 KiB.  Within a 64-position chunk a lane's rank among the lanes holding
+    // the same digit comes from one ballot per digit bit (match mask + mbcnt), so the scatter
+    // is stable without per-lane counters.
+    __device__ __noinline__ void sort_positions2(uint32_t npos_, PMC_LDS uint32_t *tab) {
+        const uint32_t npos = rfl(npos_);
+        const uint32_t l = (uint32_t)lane_id();
+        PMC_LDS uint16_t *Tt = R;
+        for (int pass = 0; pass < 2; pass++) {
+            const uint32_t sh = pass ? 8 : 0;
+            const int nb = pass ? 7 : 8;
+            PMC_LDS uint16_t *dst = pass ? S : Tt;
+            for (uint32_t k = l; k < 256; k += 64) tab[k] = 0;
+            wave_sync();
+            for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+                const uint32_t x = c0 + l;
+                const bool valid = x < npos;
+                const uint32_t p = valid ? (pass ? (uint32_t)Tt[x] : x) : 0u;
+                const uint32_t d = (hash3(load4(p)) >> sh) & 255;
+                if (valid) lds_add(&tab[d], 1u);
+            }
+            wave_sync();
+            {
+                uint32_t v[4], sum = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    v[k] = tab[4 * l + k];
+                    sum += v[k];
+                }
+                uint32_t base = wave_incl_scan(sum) - sum;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    tab[4 * l + k] = base;
+                    base += v[k];
+                }
+            }
+            wave_sync();
+            for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+                const uint32_t x = c0 + l;
+                const bool valid = x < npos;
+                const uint32_t p = valid ? (pass ? (uint32_t)Tt[x] : x) : 0u;
+                const uint32_t d = (hash3(load4(p)) >> sh) & 255;
+                uint64_t m = ballot(valid);
+                for (int bt = 0; bt < nb; bt++) {
+                    const uint64_t B = ballot((d >> bt) & 1);
+                    m &= ((d >> bt) & 1) ? B : ~B;
+                }
+                const uint32_t rank = popc_lt(m);
+                const uint32_t at = tab[d];
+                const bool last = valid && (l == 63 || (m >> (l + 1)) == 0);
+                if (valid) dst[at + rank] = (uint16_t)p;
+                if (last) tab[d] = at + rank + 1;
+                wave_sync();
             }
             wave_sync();
         }
@@ -1481,7 +1561,7 @@ struct SmallWave {
         const uint32_t npos = len >= 3 ? len - 2 : 0;
         uint32_t ntok;
         if (npos) {
-            sort_positions(npos);
+            sort_positions2(npos, (PMC_LDS uint32_t *)HC);
             stamp(1);
             ntok = parse_ondemand(npos, len);
         } else {

@@ -29,15 +29,22 @@ __device__ __forceinline__ uint64_t col_index(uint64_t v, uint32_t row) {
 }
 
 // ---- front -------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256, 4) deflate_front_kernel(DeflateArgs a) {
+__global__ void __launch_bounds__(256, 6) deflate_front_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
     const uint64_t wave = (uint64_t)blockIdx.x * wpb + wib;
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     uint8_t *base = lds + (uint64_t)wib * a.wave_bytes;
     const SmallLayout L = small_layout(a.cap_len);
+    const FrontLayout F = front_layout(a.cap_len);
     SmallWave w;
     small_wave_init(w, base, L, a, nullptr);
+    w.S = to_lds<uint16_t>(base + F.S);
+    w.R = to_lds<uint16_t>(base + F.R);
+    w.HC = to_lds<uint64_t>(base + F.X);
+    w.lfreq = to_lds<uint32_t>(base + F.freq);
+    w.dfreq = w.lfreq + 288;
+    w.blfreq = w.dfreq + 32;
     for (uint64_t g = wave * 64; g < a.count; g += nwaves * 64) {
         const uint64_t vl = g + (uint64_t)l;
         const uint32_t myl = vl < a.count ? a.src_len[a.first + vl] : 0u;
