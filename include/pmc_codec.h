@@ -122,6 +122,21 @@ int pmc_route_keys(uint64_t first, uint32_t n, uint32_t num_shards, uint32_t n_g
  * No effect otherwise. */
 int pmc_debug_stamps(pmc_ctx *ctx, uint64_t *dev_buf);
 
+/* Per-kernel launch timing (roofline diagnostics, bench.py): while enabled, every kernel the
+ * batched calls enqueue is bracketed by HIP events on its stream.  pmc_ctx_kernel_times
+ * synchronizes the context's work, adds each kind's summed milliseconds and launch count
+ * to ms[kind] / launches[kind] (kind < nkinds, indices PMC_K_*) and clears the record. */
+#define PMC_K_DEFLATE_FRONT 0 /* split pipeline: stage, hash sort, lazy parse, histograms */
+#define PMC_K_DEFLATE_TREES 1 /* split pipeline: lane-parallel Huffman trees + block plan */
+#define PMC_K_DEFLATE_BACK 2  /* split pipeline: CRC, codes, emission, framing           */
+#define PMC_K_DEFLATE_MONO 3  /* single-kernel small-value deflate (PMC_DEFLATE_MONO=1)  */
+#define PMC_K_DEFLATE_HBM 4   /* values > 16382 B                                       */
+#define PMC_K_INFLATE_LDS 5
+#define PMC_K_INFLATE_HBM 6
+#define PMC_K_COUNT 8
+int pmc_ctx_profile(pmc_ctx *ctx, int enable);
+int pmc_ctx_kernel_times(pmc_ctx *ctx, double *ms, uint32_t *launches, int nkinds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,6 +6,8 @@
 // the rest (large values; same device code, working set in a per-wave HBM slab).
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstdio>
@@ -148,12 +150,36 @@ struct pmc_ctx {
     DevBuf tokens, dscratch;     // deflate symbol slabs / HBM working sets
     DevBuf fbscratch;            // per-wave Trees for the small kernel's serial fallback
     DevBuf split;                // chunk arrays of the split small-value pipeline
+    bool prof = false;           // pmc_ctx_profile: bracket every launch with events
+    struct KRec {
+        int kind;
+        hipEvent_t a, b;
+    };
+    std::vector<KRec> krecs;
     DevBuf staging;              // device side of host-API calls
     uint64_t *dbg = nullptr;     // diagnostic stamp sums (PMC_STAMPS builds)
     HostBuf pinned;              // host side of host-API calls
 };
 
 namespace {
+
+// Runs `launch` (which enqueues one kernel on st); with profiling on, brackets it with events.
+template <class F>
+void klaunch(pmc_ctx *ctx, int kind, hipStream_t st, F launch) {
+    if (!ctx->prof) {
+        launch();
+        return;
+    }
+    pmc_ctx::KRec r{kind, nullptr, nullptr};
+    if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) {
+        launch();
+        return;
+    }
+    (void)hipEventRecord(r.a, st);
+    launch();
+    (void)hipEventRecord(r.b, st);
+    ctx->krecs.push_back(r);
+}
 
 struct Launch {
     int wpb;        // waves per block
@@ -263,6 +289,11 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     c->dscratch.release();
     c->fbscratch.release();
     c->split.release();
+    for (auto &r : c->krecs) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    c->krecs.clear();
     c->staging.release();
     c->pinned.release();
     (void)hipStreamDestroy(c->stream);
@@ -356,17 +387,23 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
             a.count = std::min<uint64_t>(chunk, n - first);
             const unsigned tb = (unsigned)((a.count + 63) / 64);
             a.wave_bytes = fwb;
-            hipLaunchKernelGGL(deflate_front_kernel,
-                               dim3((unsigned)std::min<uint64_t>(Lf.blocks, (a.count + Lf.wpb - 1) / Lf.wpb)),
-                               dim3(64 * Lf.wpb), Lf.lds - kCrcTabBytes, st, a);
+            klaunch(ctx, PMC_K_DEFLATE_FRONT, st, [&] {
+                hipLaunchKernelGGL(deflate_front_kernel,
+                                   dim3((unsigned)std::min<uint64_t>(Lf.blocks, (a.count + Lf.wpb - 1) / Lf.wpb)),
+                                   dim3(64 * Lf.wpb), Lf.lds - kCrcTabBytes, st, a);
+            });
             if (hipMemsetAsync(a.cD + a.count, 0, 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
-            hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap>, dim3(tb), dim3(64), tl_small, st, a);
-            hipLaunchKernelGGL(deflate_trees_kernel<kLCodes>, dim3(std::min<unsigned>(tb, (unsigned)ctx->cus)), dim3(64),
-                               tl_big, st, a);
+            klaunch(ctx, PMC_K_DEFLATE_TREES, st, [&] {
+                hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap>, dim3(tb), dim3(64), tl_small, st, a);
+                hipLaunchKernelGGL(deflate_trees_kernel<kLCodes>, dim3(std::min<unsigned>(tb, (unsigned)ctx->cus)),
+                                   dim3(64), tl_big, st, a);
+            });
             a.wave_bytes = bwb;
-            hipLaunchKernelGGL(deflate_back_kernel,
-                               dim3((unsigned)std::min<uint64_t>(Lb.blocks, (a.count + Lb.wpb - 1) / Lb.wpb)),
-                               dim3(64 * Lb.wpb), Lb.lds, st, a);
+            klaunch(ctx, PMC_K_DEFLATE_BACK, st, [&] {
+                hipLaunchKernelGGL(deflate_back_kernel,
+                                   dim3((unsigned)std::min<uint64_t>(Lb.blocks, (a.count + Lb.wpb - 1) / Lb.wpb)),
+                                   dim3(64 * Lb.wpb), Lb.lds, st, a);
+            });
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
@@ -392,8 +429,10 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
         a.cap_len = cap;
         a.wave_bytes = lds_wb;
         a.scratch = (uint8_t *)ctx->fbscratch.p;
-        if (force_v1) hipLaunchKernelGGL(deflate_kernel<false>, dim3(Ls.blocks), dim3(64 * Ls.wpb), Ls.lds, st, a);
-        else hipLaunchKernelGGL(deflate_small_kernel, dim3(Ls.blocks), dim3(64 * Ls.wpb), Ls.lds, st, a);
+        klaunch(ctx, PMC_K_DEFLATE_MONO, st, [&] {
+            if (force_v1) hipLaunchKernelGGL(deflate_kernel<false>, dim3(Ls.blocks), dim3(64 * Ls.wpb), Ls.lds, st, a);
+            else hipLaunchKernelGGL(deflate_small_kernel, dim3(Ls.blocks), dim3(64 * Ls.wpb), Ls.lds, st, a);
+        });
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
             set_err("deflate_kernel<lds>", e);
@@ -406,7 +445,9 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
         a.cap_len = max_len;
         a.wave_bytes = hbm_wb;
         a.scratch = (uint8_t *)ctx->dscratch.p;
-        hipLaunchKernelGGL(deflate_kernel<true>, dim3((unsigned)hbm_waves), dim3(64), kCrcTabBytes, st, a);
+        klaunch(ctx, PMC_K_DEFLATE_HBM, st, [&] {
+            hipLaunchKernelGGL(deflate_kernel<true>, dim3((unsigned)hbm_waves), dim3(64), kCrcTabBytes, st, a);
+        });
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
             set_err("deflate_kernel<hbm>", e);
@@ -436,7 +477,8 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
         uint64_t wb = inflate_wave_bytes(false, a.lds_max_out, a.lds_max_in);
         Launch L = plan_lds(ctx, (const void *)inflate_kernel<false>, wb, n);
         a.wave_bytes = wb;
-        hipLaunchKernelGGL(inflate_kernel<false>, dim3(L.blocks), dim3(64 * L.wpb), L.lds, st, a);
+        klaunch(ctx, PMC_K_INFLATE_LDS, st,
+                [&] { hipLaunchKernelGGL(inflate_kernel<false>, dim3(L.blocks), dim3(64 * L.wpb), L.lds, st, a); });
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
             set_err("inflate_kernel<lds>", e);
@@ -450,8 +492,10 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
         uint64_t wb = inflate_wave_bytes(true, 0, 0);
         uint64_t waves = std::min<uint64_t>((uint64_t)ctx->cus * 4, n);
         a.wave_bytes = wb;
-        hipLaunchKernelGGL(inflate_kernel<true>, dim3((unsigned)((waves + 3) / 4)), dim3(256),
-                           kCrcTabBytes + 4 * wb, st, a);
+        klaunch(ctx, PMC_K_INFLATE_HBM, st, [&] {
+            hipLaunchKernelGGL(inflate_kernel<true>, dim3((unsigned)((waves + 3) / 4)), dim3(256),
+                               kCrcTabBytes + 4 * wb, st, a);
+        });
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
             set_err("inflate_kernel<hbm>", e);
@@ -459,6 +503,29 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
         }
     }
     return PMC_OK;
+}
+
+PMC_API int pmc_ctx_profile(pmc_ctx *ctx, int enable) {
+    if (!ctx) return PMC_E_ARG;
+    ctx->prof = enable != 0;
+    return PMC_OK;
+}
+
+PMC_API int pmc_ctx_kernel_times(pmc_ctx *ctx, double *ms, uint32_t *launches, int nkinds) {
+    if (!ctx || !ms || !launches || nkinds < 0) return PMC_E_ARG;
+    int rc = PMC_OK;
+    for (auto &r : ctx->krecs) {
+        float t = 0;
+        if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&t, r.a, r.b) != hipSuccess) rc = PMC_E_NO_DEVICE;
+        if (r.kind < nkinds) {
+            ms[r.kind] += t;
+            launches[r.kind] += 1;
+        }
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    ctx->krecs.clear();
+    return rc;
 }
 
 PMC_API int pmc_gzip_isize_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,

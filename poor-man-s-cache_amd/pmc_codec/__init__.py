@@ -62,7 +62,17 @@ SIGNATURES = {
     "pmc_compare_values": (_c.c_int, [_p, _p, _p, _p, _p, _p, _u32, _p, _p]),
     "pmc_route_keys": (_c.c_int, [_u64, _u32, _u32, _u32, _p, _p]),
     "pmc_debug_stamps": (_c.c_int, [_p, _p]),
+    "pmc_ctx_profile": (_c.c_int, [_p, _c.c_int]),
+    "pmc_ctx_kernel_times": (_c.c_int, [_p, _c.POINTER(_c.c_double), _c.POINTER(_u32), _c.c_int]),
 }
+
+# pmc_ctx_kernel_times kinds (include/pmc_codec.h PMC_K_*)
+KERNEL_KINDS = ["deflate_front", "deflate_trees", "deflate_back", "deflate_mono", "deflate_hbm", "inflate_lds",
+                "inflate_hbm", "-"]
+KERNEL_NAMES = {"deflate_front": "pmc::deflate_front_kernel", "deflate_trees": "pmc::deflate_trees_kernel",
+                "deflate_back": "pmc::deflate_back_kernel", "deflate_mono": "pmc::deflate_small_kernel",
+                "deflate_hbm": "pmc::deflate_kernel<true>", "inflate_lds": "pmc::inflate_kernel<false>",
+                "inflate_hbm": "pmc::inflate_kernel<true>"}
 
 
 def lib():
@@ -105,6 +115,20 @@ class Context:
         if rc != 0:
             raise CodecUnavailable(f"pmc_ctx_create({device}) = {rc}: {last_error()}")
         self.device = device
+
+    def profile(self, enable: bool):
+        """Bracket every kernel the batched calls enqueue with HIP events (diagnostics)."""
+        lib().pmc_ctx_profile(self.handle, 1 if enable else 0)
+
+    def kernel_times(self):
+        """{kind: (total_ms, launches)} of the launches recorded since profile(True)."""
+        n = len(KERNEL_KINDS)
+        ms = (ctypes.c_double * n)()
+        cnt = (_u32 * n)()
+        rc = lib().pmc_ctx_kernel_times(self.handle, ms, cnt, n)
+        if rc != 0:
+            raise CodecUnavailable(f"pmc_ctx_kernel_times failed ({rc}): {last_error()}")
+        return {KERNEL_KINDS[k]: (ms[k], cnt[k]) for k in range(n) if cnt[k]}
 
     def close(self):
         if self.handle:

@@ -34,13 +34,13 @@ def main():
         cal = 2.0 * avg(fe["pmc::compare_values_kernel"]) / known
     res = {"n": n, "vlen": vlen, "kind": kind, "fetch_correction": 2.0, "fetch_calibration": cal,
            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, bench.py workload"}
-    for k, key in (("pmc::deflate_small_kernel", "deflate"), ("pmc::inflate_kernel<false>", "inflate")):
-        f, w = avg(fe.get(k, [])), avg(wr.get(k, []))
-        if f is None or w is None:
+    res["kernels"] = {}
+    for k in sorted(set(fe) & set(wr)):
+        if not k.startswith("pmc::"):
             continue
-        res[f"{key}_fetch_bytes_per_launch"] = 2.0 * f
-        res[f"{key}_write_bytes_per_launch"] = w
-        res[f"{key}_hbm_bytes_per_launch"] = 2.0 * f + w
+        f, w = avg(fe[k]), avg(wr[k])
+        res["kernels"][k] = {"launches": len(fe[k]), "fetch_bytes_per_launch": 2.0 * f,
+                             "write_bytes_per_launch": w, "hbm_bytes_per_launch": 2.0 * f + w}
     print(json.dumps(res, indent=1))
 
 
