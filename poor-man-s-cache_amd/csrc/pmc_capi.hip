@@ -150,6 +150,7 @@ struct pmc_ctx {
     DevBuf tokens, dscratch;     // deflate symbol slabs / HBM working sets
     DevBuf fbscratch;            // per-wave Trees for the small kernel's serial fallback
     DevBuf split;                // chunk arrays of the split small-value pipeline
+    DevBuf crcx;                 // inflate: CRC-32 trailers from the lane kernel
     bool prof = false;           // pmc_ctx_profile: bracket every launch with events
     struct KRec {
         int kind;
@@ -289,6 +290,7 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     c->dscratch.release();
     c->fbscratch.release();
     c->split.release();
+    c->crcx.release();
     for (auto &r : c->krecs) {
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
@@ -466,7 +468,24 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
     hipStream_t st = (hipStream_t)stream;
-    InflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, ctx->dbg ? ctx->dbg + 16 : nullptr};
+    InflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, ctx->dbg ? ctx->dbg + 16 : nullptr,
+                  nullptr, 0};
+    // lane-per-member fast path (pmc_inflate_lane.hip), then the CRC check; whatever it
+    // declines (rc = kInflateRetry) goes through the wave-per-member kernels below
+    // (PMC_INFLATE_WAVE=1: everything through the wave kernels).
+    static const bool wave_only = getenv("PMC_INFLATE_WAVE") && atoi(getenv("PMC_INFLATE_WAVE"));
+    if (!wave_only) {
+        int r = ctx->crcx.ensure((uint64_t)n * 4);
+        if (r) return r;
+        a.crc_expect = (uint32_t *)ctx->crcx.p;
+        const unsigned lb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * 16);
+        klaunch(ctx, PMC_K_INFLATE_LANE, st,
+                [&] { hipLaunchKernelGGL(inflate_lane_kernel, dim3(lb), dim3(64), kLaneLdsBytes, st, a); });
+        const unsigned vb = (unsigned)std::min<uint64_t>(((uint64_t)n + 255) / 256, (uint64_t)ctx->cus * 8);
+        klaunch(ctx, PMC_K_INFLATE_VERIFY, st,
+                [&] { hipLaunchKernelGGL(inflate_verify_kernel, dim3(vb), dim3(256), 0, st, a); });
+        a.retry_only = 1;
+    }
     // output image capacity for the LDS kernel; the compressed input of a member whose
     // output fits is at most gzip_bound(out) unless it is not a deflate member at all
     uint64_t out_cap = std::min<uint64_t>(inflate_lds_out_limit(), std::max<uint64_t>(max_len, 1));

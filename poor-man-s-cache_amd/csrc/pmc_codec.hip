@@ -4,5 +4,6 @@
 #include "pmc_deflate_small.hip"
 #include "pmc_deflate_split.hip"
 #include "pmc_inflate.hip"
+#include "pmc_inflate_lane.hip"
 #include "pmc_misc.hip"
 #include "pmc_capi.hip"

@@ -1120,7 +1120,8 @@ __global__ void __launch_bounds__(256, 5) inflate_kernel(InflateArgs a) {
             my_cap = a.dst_cap[vl];
         }
         const bool my_fits = my_cap <= a.lds_max_out && my_in <= a.lds_max_in;
-        uint64_t todo = ballot(vl < a.n && (kHbm != my_fits));
+        const bool mine = vl < a.n && (!a.retry_only || a.rc[vl] == kInflateRetry);
+        uint64_t todo = ballot(mine && (kHbm != my_fits));
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;

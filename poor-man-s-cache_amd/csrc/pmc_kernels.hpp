@@ -74,7 +74,11 @@ struct InflateArgs {
     uint64_t wave_bytes;
     uint8_t *scratch;
     uint64_t *dbg; // PMC_STAMPS builds: per-phase cycle sums (slots 0..7 deflate-independent)
+    uint32_t *crc_expect; // lane kernel -> verify kernel: the member's CRC-32 trailer
+    int32_t retry_only;   // wave kernels: only members the lane kernel marked kInflateRetry
 };
+
+constexpr int32_t kInflateRetry = -7777; // internal rc: lane fast path declined the member
 
 uint64_t deflate_wave_bytes(bool hbm, uint64_t n);
 uint64_t deflate_small_wave_bytes(uint64_t n);
@@ -91,5 +95,7 @@ __global__ void deflate_trees_kernel(DeflateArgs a);
 __global__ void deflate_back_kernel(DeflateArgs a);
 template <bool kHbm>
 __global__ void inflate_kernel(InflateArgs a);
+__global__ void inflate_lane_kernel(InflateArgs a);
+__global__ void inflate_verify_kernel(InflateArgs a);
 
 } // namespace pmc

@@ -23,8 +23,11 @@ def main():
                      data.data_ptr(), D.stream_handle())
     off = torch.arange(n, dtype=torch.int64, device="cuda") * vlen
     lens = torch.full((n,), vlen, dtype=torch.int32, device="cuda")
-    D.compress(ctx, D.Batch(data, off, lens, n, vlen))
+    out, rc = D.compress(ctx, D.Batch(data, off, lens, n, vlen))
     torch.cuda.synchronize()
+    if os.environ.get("PMC_DRIVE_DECOMPRESS"):
+        D.decompress(ctx, out, [vlen] * n)
+        torch.cuda.synchronize()
     ctx.close()
 
 
