@@ -26,19 +26,18 @@
 
 namespace pmc {
 
-constexpr int kLaneLitCap = 128, kLaneDistCap = 32;
-// per-lane LDS columns (u16 words): symbol lists, code-length code list, counts/offsets, bases
-constexpr int kColLit = 0, kColDist = kColLit + kLaneLitCap, kColCl = kColDist + kLaneDistCap;
-constexpr int kColCntL = kColCl + 19, kColCntD = kColCntL + 16, kColBaseL = kColCntD + 16;
-constexpr int kColBaseD = kColBaseL + 16, kColBaseC = kColBaseD + 16, kColWords = kColBaseC + 8;
-constexpr uint32_t kLaneTabOff = (uint32_t)kColWords * 64 * 2;     // length/distance base tables
-constexpr uint32_t kLaneLdsBytes = kLaneTabOff + 64 * 4;
+constexpr int kLaneLitCap = 96, kLaneDistCap = 32;
+// per-lane LDS columns (u16 words, entry i of lane l at word i * 64 + l).  Decode-time:
+// symbol lists and bases.  Build-time scratch (counts / offsets, code-length code) lives in
+// the output ring's bytes, which are only written once decoding starts.
+constexpr int kColLit = 0, kColDist = kColLit + kLaneLitCap, kColBaseL = kColDist + kLaneDistCap;
+constexpr int kColBaseD = kColBaseL + 16, kColWords = kColBaseD + 16;
+constexpr int kBColCntL = 0, kBColCntD = 16, kBColBaseC = 32, kBColCl = 40; // build columns
+constexpr uint32_t kLaneTabOff = (uint32_t)kColWords * 64 * 2;             // length/distance bases
+constexpr uint32_t kLaneRingOff = (kLaneTabOff + 64 * 4 + 255) & ~255u;    // output rings (LaneOut)
+constexpr uint32_t kLaneWinOff = kLaneRingOff + 256 / 4 * 64 * 4;          // input windows (LaneWin)
+constexpr uint32_t kLaneLdsBytes = kLaneWinOff + 32 * 64 * 4;
 
-// Bit reader over a member in HBM.  Input arrives as aligned 16-byte blocks, one block
-// ahead of the one being consumed, so the load a refill depends on was issued ~4 refills
-// earlier (loads and stores share vmcnt on gfx9: an immediately-used load would also wait
-// for every output byte stored before it).  Aligned blocks never cross a page, so reading
-// the tail of the last one is safe.
 struct LaneIn {
     const uint8_t *p;
     uint32_t len;       // member bytes
@@ -96,6 +95,73 @@ struct LaneIn {
     }
 };
 
+// Bit reader of the decode loop: the next 32 dwords of the member sit in an LDS window
+// (column layout, stream dword j at slot j & 31).  Windows advance by 16 dwords for every
+// lane that can at the same time (wave-synchronous refill), so the wave waits on global
+// loads a few times per member instead of whenever any one lane's buffer runs low.
+struct LaneWin {
+    PMC_LDS uint32_t *w; // slot s at w[s * 64]
+    const uint4 *blk;    // member rounded down to 16 bytes
+    uint32_t nblk;       // blocks holding member bytes
+    uint32_t head;       // member start - blk, in bits
+    uint32_t wlo;        // first dword held
+    uint32_t nd;         // next dword to move into buf
+    uint64_t buf;
+    uint32_t n;
+    __device__ uint4 block(uint32_t k) const { return k < nblk ? blk[k] : make_uint4(0, 0, 0, 0); }
+    __device__ void load16(uint32_t d0) { // dwords d0 .. d0 + 15 (d0 % 16 == 0) into their slots
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const uint4 x = block(d0 / 4 + b);
+            const uint32_t s0 = (d0 + 4 * b) & 31;
+            w[(s0 + 0) * 64] = x.x;
+            w[(s0 + 1) * 64] = x.y;
+            w[(s0 + 2) * 64] = x.z;
+            w[(s0 + 3) * 64] = x.w;
+        }
+    }
+    __device__ void start(const LaneIn &in, uint64_t bp) { // at member bit bp
+        blk = in.blk;
+        head = (uint32_t)(((uintptr_t)in.p & 15) * 8);
+        nblk = (uint32_t)((((uintptr_t)in.p & 15) + in.len + 15) / 16);
+        const uint64_t a = bp + head;
+        nd = (uint32_t)(a >> 5);
+        wlo = nd & ~15u;
+        load16(wlo);
+        load16(wlo + 16);
+        buf = 0;
+        n = 0;
+        refill();
+        drop((uint32_t)(a & 31));
+    }
+    __device__ void refill() {
+        if (n <= 32) {
+            buf |= (uint64_t)w[(nd & 31) * 64] << n;
+            n += 32;
+            nd++;
+        }
+    }
+    __device__ bool needs() const { return nd + 4 > wlo + 32; }
+    __device__ void advance() { // retire the older half of the window if it is consumed
+        if (nd >= wlo + 16) {
+            load16(wlo + 32);
+            wlo += 16;
+        }
+    }
+    __device__ uint32_t peek(uint32_t k) const { return (uint32_t)buf & ((1u << k) - 1); }
+    __device__ void drop(uint32_t k) {
+        buf >>= k;
+        n -= k;
+    }
+    __device__ uint32_t bits(uint32_t k) {
+        refill();
+        const uint32_t v = peek(k);
+        drop(k);
+        return v;
+    }
+    __device__ uint64_t bitpos() const { return (uint64_t)nd * 32 - n - head; }
+};
+
 // One canonical code of up to 15-bit lengths: per-length limits in registers, bases and the
 // sorted symbol list in the lane's LDS column.
 template <int NL>
@@ -119,7 +185,8 @@ struct LaneCode {
         }
         return left == 0;
     }
-    __device__ uint32_t decode(LaneIn &in) const {
+    template <class R>
+    __device__ uint32_t decode(R &in) const {
         const uint32_t x = __builtin_bitreverse32(in.peek(15)) >> 17;
         uint32_t L = 1;
 #pragma unroll
@@ -130,7 +197,8 @@ struct LaneCode {
     }
 };
 
-__device__ __forceinline__ uint32_t fixed_lit(LaneIn &in) {
+template <class R>
+__device__ __forceinline__ uint32_t fixed_lit(R &in) {
     const uint32_t x9 = __builtin_bitreverse32(in.peek(9)) >> 23;
     uint32_t sym, len;
     if ((x9 >> 2) < 24) {
@@ -154,7 +222,7 @@ __device__ __forceinline__ uint32_t fixed_lit(LaneIn &in) {
 // (cnt columns), pass 1 places every symbol into its list (cnt columns hold offsets).
 // Returns false on any malformed sequence.
 __device__ bool lane_lengths(LaneIn &in, const LaneCode<7> &clc, uint32_t nlen, uint32_t nlit, PMC_LDS uint16_t *col,
-                             int pass, bool &eob_ok) {
+                             PMC_LDS uint16_t *bcol, int pass, bool &eob_ok) {
     uint32_t k = 0, prev = 0;
     while (k < nlen) {
         in.refill();
@@ -178,7 +246,7 @@ __device__ bool lane_lengths(LaneIn &in, const LaneCode<7> &clc, uint32_t nlen, 
         if (val) {
             for (uint32_t r = 0; r < rep; r++, k++) {
                 const bool lit = k < nlit;
-                PMC_LDS uint16_t *c = col + (lit ? kColCntL : kColCntD) * 64 + val * 64;
+                PMC_LDS uint16_t *c = bcol + (lit ? kBColCntL : kBColCntD) * 64 + val * 64;
                 if (pass == 0) {
                     *c = (uint16_t)(*c + 1);
                     if (k == 256) eob_ok = true;
@@ -196,179 +264,254 @@ __device__ bool lane_lengths(LaneIn &in, const LaneCode<7> &clc, uint32_t nlen, 
     return true;
 }
 
-__device__ void lane_copy(uint8_t *out, uint32_t pos, uint32_t dist, uint32_t len, uint32_t cap) {
-    if (dist >= 8) {
-        uint32_t k = 0;
-        for (; k < len && pos + k + 4 <= cap; k += 8) {
-            const uintptr_t a = (uintptr_t)(out + pos - dist + k);
-            const uint32_t *q = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
-            const uint32_t sh = (uint32_t)(a & 3);
-            const uint32_t q0 = q[0], q1 = q[1], q2 = q[2];
-            const uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(q2, q1, sh) << 32 | __builtin_amdgcn_alignbyte(q1, q0, sh);
-            const uint32_t m = len - k < 8 ? len - k : 8;
-#pragma unroll
-            for (uint32_t j = 0; j < 8; j++)
-                if (j < m) out[pos + k + j] = (uint8_t)(v >> (8 * j));
+// Header and block header of a single-block fixed/dynamic member, code tables built;
+// false = decline (stored or multi-block members, header flags, malformed codes ...).
+__device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint16_t *bcol, LaneCode<15> &lit,
+                             LaneCode<15> &dist, bool &fixed) {
+    if (in.len < 18) return false;
+    if (in.byte_at(0) != 0x1f || in.byte_at(1) != 0x8b || in.byte_at(2) != 8 || in.byte_at(3) != 0) return false;
+    in.seek(80);
+    const uint32_t bfinal = in.bits(1), btype = in.bits(2);
+    if (!bfinal || btype == 0 || btype == 3) return false;
+    fixed = btype == 1;
+    if (fixed) return true;
+    const uint32_t nlit = in.bits(5) + 257, ndist = in.bits(5) + 1, ncl = in.bits(4) + 4;
+    if (nlit > 286 || ndist > 30) return false;
+    // code-length code: lengths (3 bits each, permuted order), counts, list
+    uint64_t cll = 0;
+    for (uint32_t k = 0; k < ncl; k++) cll |= (uint64_t)in.bits(3) << (3 * c_cl_order[k]);
+    for (int L = 0; L < 16; L++) bcol[(kBColCntL + L) * 64] = 0;
+    for (uint32_t sy = 0; sy < 19; sy++) {
+        const uint32_t L = (uint32_t)(cll >> (3 * sy)) & 7;
+        if (L) bcol[(kBColCntL + L) * 64] = (uint16_t)(bcol[(kBColCntL + L) * 64] + 1);
+    }
+    LaneCode<7> clc;
+    clc.base = (PMC_LDS int16_t *)(bcol + kBColBaseC * 64);
+    clc.sym = bcol + kBColCl * 64;
+    if (!clc.build(bcol + kBColCntL * 64)) return false;
+    {
+        uint32_t offs = 0;
+        for (int L = 1; L < 8; L++) {
+            const uint32_t c = bcol[(kBColCntL + L) * 64];
+            bcol[(kBColCntL + L) * 64] = (uint16_t)offs;
+            offs += c;
         }
-        for (; k < len; k++) out[pos + k] = out[pos - dist + k]; // (last bytes of dst: no over-read)
-    } else {
-        uint64_t pat = 0;
-        for (uint32_t j = 0; j < dist; j++) pat |= (uint64_t)out[pos - dist + j] << (8 * j);
-        uint32_t idx = 0;
-        for (uint32_t k = 0; k < len; k++) {
-            out[pos + k] = (uint8_t)(pat >> (8 * idx));
-            idx = idx + 1 == dist ? 0 : idx + 1;
+        for (uint32_t sy = 0; sy < 19; sy++) {
+            const uint32_t L = (uint32_t)(cll >> (3 * sy)) & 7;
+            if (L) {
+                const uint32_t at = bcol[(kBColCntL + L) * 64];
+                bcol[(kBColCntL + L) * 64] = (uint16_t)(at + 1);
+                clc.sym[at * 64] = (uint16_t)sy;
+            }
         }
     }
+    // pass 0: counts of the literal/length and distance codes
+    for (int L = 0; L < 16; L++) {
+        bcol[(kBColCntL + L) * 64] = 0;
+        bcol[(kBColCntD + L) * 64] = 0;
+    }
+    const uint64_t lens_at = in.bitpos();
+    bool eob_ok = false;
+    if (!lane_lengths(in, clc, nlit + ndist, nlit, col, bcol, 0, eob_ok) || !eob_ok) return false;
+    const uint64_t data_at = in.bitpos();
+    uint32_t nl = 0, nd = 0;
+    for (int L = 1; L < 16; L++) {
+        nl += bcol[(kBColCntL + L) * 64];
+        nd += bcol[(kBColCntD + L) * 64];
+    }
+    if (nl > (uint32_t)kLaneLitCap || nd > (uint32_t)kLaneDistCap) return false;
+    if (!lit.build(bcol + kBColCntL * 64) || !dist.build(bcol + kBColCntD * 64)) return false;
+    {
+        uint32_t ol = 0, od = 0;
+        for (int L = 1; L < 16; L++) {
+            const uint32_t cl = bcol[(kBColCntL + L) * 64], cd = bcol[(kBColCntD + L) * 64];
+            bcol[(kBColCntL + L) * 64] = (uint16_t)ol;
+            bcol[(kBColCntD + L) * 64] = (uint16_t)od;
+            ol += cl;
+            od += cd;
+        }
+    }
+    in.seek(lens_at);
+    lane_lengths(in, clc, nlit + ndist, nlit, col, bcol, 1, eob_ok);
+    in.seek(data_at);
+    return true;
 }
 
-// Decodes one member; returns 0 (output written, CRC still to check) or kInflateRetry.
-__device__ int lane_inflate(LaneIn &in, uint8_t *out, uint32_t cap, PMC_LDS uint16_t *col,
-                            PMC_LDS const uint32_t *ltab, PMC_LDS const uint32_t *dtab, uint32_t *out_len,
-                            uint32_t *crc_expect) {
-    if (in.len < 18) return kInflateRetry;
-    if (in.byte_at(0) != 0x1f || in.byte_at(1) != 0x8b || in.byte_at(2) != 8 || in.byte_at(3) != 0) return kInflateRetry;
-    in.seek(80);
-    LaneCode<15> lit, dist;
-    lit.base = (PMC_LDS int16_t *)(col + kColBaseL * 64);
-    lit.sym = col + kColLit * 64;
-    dist.base = (PMC_LDS int16_t *)(col + kColBaseD * 64);
-    dist.sym = col + kColDist * 64;
-    uint32_t pos = 0, bfinal;
-    do {
-        bfinal = in.bits(1);
-        const uint32_t btype = in.bits(2);
-        if (btype == 0) {
-            uint64_t bp = (in.bitpos() + 7) & ~(uint64_t)7;
-            const uint32_t o = (uint32_t)(bp >> 3);
-            if (o + 4 > in.len) return kInflateRetry;
-            const uint32_t L = in.byte_at(o) | in.byte_at(o + 1) << 8, NL = in.byte_at(o + 2) | in.byte_at(o + 3) << 8;
-            if ((L ^ 0xffffu) != NL || o + 4 + L > in.len || pos + L > cap) return kInflateRetry;
-            for (uint32_t k = 0; k < L; k++) out[pos + k] = in.p[o + 4 + k];
-            pos += L;
-            in.seek((uint64_t)(o + 4 + L) * 8);
-            continue;
+// Output of one lane: the last kRing bytes live in an LDS ring (column layout, dword k of
+// the ring at word k * 64 of the lane's column) aligned so that ring dwords map onto dst
+// dwords; complete dwords go to dst in bursts of >= kFlush bytes.  Keeping the byte-level
+// traffic in LDS keeps vmcnt free of thousands of byte stores (on gfx9 loads and stores
+// share it, so every later load would wait for them).
+constexpr uint32_t kRing = 256, kFlush = 128;
+struct LaneOut {
+    PMC_LDS uint8_t *rb;  // byte view of the lane's ring column (byte q at (q >> 2) * 256 + (q & 3))
+    PMC_LDS uint32_t *rw; // dword view (dword k at k * 64)
+    uint32_t *dw;         // dst rounded down to 4 bytes
+    uint8_t *dst;
+    uint32_t a0;          // dst & 3
+    uint32_t pos, flushed; // bytes produced / bytes in dst
+    __device__ void put(uint32_t p, uint32_t b) {
+        const uint32_t q = (p + a0) & (kRing - 1);
+        rb[(q >> 2) * 256 + (q & 3)] = (uint8_t)b;
+    }
+    __device__ uint32_t ringw(uint32_t k) const { return rw[(k & (kRing / 4 - 1)) * 64]; }
+    // 8 bytes starting at output position src (all of them already produced)
+    __device__ uint64_t get8(uint32_t src, bool from_ring) const {
+        const uint32_t q = src + a0, k = q >> 2, sh = q & 3;
+        uint32_t w0, w1, w2;
+        if (from_ring) {
+            w0 = ringw(k);
+            w1 = ringw(k + 1);
+            w2 = ringw(k + 2);
+        } else {
+            w0 = dw[k];
+            w1 = dw[k + 1];
+            w2 = dw[k + 2];
         }
-        if (btype == 3) return kInflateRetry;
-        const bool fixed = btype == 1;
-        if (!fixed) {
-            const uint32_t nlit = in.bits(5) + 257, ndist = in.bits(5) + 1, ncl = in.bits(4) + 4;
-            if (nlit > 286 || ndist > 30) return kInflateRetry;
-            // code-length code: lengths (3 bits each, permuted order), counts, list
-            uint64_t cll = 0;
-            for (uint32_t k = 0; k < ncl; k++) cll |= (uint64_t)in.bits(3) << (3 * c_cl_order[k]);
-            for (int L = 0; L < 16; L++) col[(kColCntL + L) * 64] = 0;
-            for (uint32_t s = 0; s < 19; s++) {
-                const uint32_t L = (uint32_t)(cll >> (3 * s)) & 7;
-                if (L) col[(kColCntL + L) * 64] = (uint16_t)(col[(kColCntL + L) * 64] + 1);
-            }
-            LaneCode<7> clc;
-            clc.base = (PMC_LDS int16_t *)(col + kColBaseC * 64);
-            clc.sym = col + kColCl * 64;
-            if (!clc.build(col + kColCntL * 64)) return kInflateRetry;
-            {
-                uint32_t offs = 0;
-                for (int L = 1; L < 8; L++) {
-                    const uint32_t c = col[(kColCntL + L) * 64];
-                    col[(kColCntL + L) * 64] = (uint16_t)offs;
-                    offs += c;
-                }
-                for (uint32_t s = 0; s < 19; s++) {
-                    const uint32_t L = (uint32_t)(cll >> (3 * s)) & 7;
-                    if (L) {
-                        const uint32_t at = col[(kColCntL + L) * 64];
-                        col[(kColCntL + L) * 64] = (uint16_t)(at + 1);
-                        clc.sym[at * 64] = (uint16_t)s;
-                    }
-                }
-            }
-            // pass 0: counts of the literal/length and distance codes
-            for (int L = 0; L < 16; L++) {
-                col[(kColCntL + L) * 64] = 0;
-                col[(kColCntD + L) * 64] = 0;
-            }
-            const uint64_t lens_at = in.bitpos();
-            bool eob_ok = false;
-            if (!lane_lengths(in, clc, nlit + ndist, nlit, col, 0, eob_ok) || !eob_ok) return kInflateRetry;
-            const uint64_t data_at = in.bitpos();
-            uint32_t nl = 0, nd = 0;
-            for (int L = 1; L < 16; L++) {
-                nl += col[(kColCntL + L) * 64];
-                nd += col[(kColCntD + L) * 64];
-            }
-            if (nl > (uint32_t)kLaneLitCap || nd > (uint32_t)kLaneDistCap) return kInflateRetry;
-            if (!lit.build(col + kColCntL * 64) || !dist.build(col + kColCntD * 64)) return kInflateRetry;
-            // counts -> running offsets, pass 1: place the symbols
-            {
-                uint32_t ol = 0, od = 0;
-                for (int L = 1; L < 16; L++) {
-                    const uint32_t cl = col[(kColCntL + L) * 64], cd = col[(kColCntD + L) * 64];
-                    col[(kColCntL + L) * 64] = (uint16_t)ol;
-                    col[(kColCntD + L) * 64] = (uint16_t)od;
-                    ol += cl;
-                    od += cd;
-                }
-            }
-            in.seek(lens_at);
-            lane_lengths(in, clc, nlit + ndist, nlit, col, 1, eob_ok);
-            in.seek(data_at);
+        return (uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32 | __builtin_amdgcn_alignbyte(w1, w0, sh);
+    }
+    // write every complete dword below position `upto` (all bytes when `last`)
+    __device__ void flush(uint32_t upto, bool last) {
+        if (flushed == 0 && a0 && upto > 0) { // head dword: only the member's own bytes
+            const uint32_t h = 4 - a0 < upto ? 4 - a0 : upto;
+            for (uint32_t j = 0; j < h; j++) dst[j] = rb[((a0 + j) & (kRing - 1)) / 4 * 256 + ((a0 + j) & 3)];
+            flushed = h;
         }
-        for (;;) {
-            in.refill();
-            const uint32_t s = fixed ? fixed_lit(in) : lit.decode(in);
-            if (s < 256) {
-                if (pos >= cap) return kInflateRetry;
-                out[pos++] = (uint8_t)s;
-                continue;
+        const uint32_t k1 = (upto + a0) >> 2;
+        for (uint32_t k = (flushed + a0) >> 2; k < k1; k++) dw[k] = ringw(k);
+        if (k1 * 4 > flushed + a0) flushed = k1 * 4 - a0;
+        if (last) {
+            for (uint32_t p = flushed; p < upto; p++) {
+                const uint32_t q = (p + a0) & (kRing - 1);
+                dst[p] = rb[(q >> 2) * 256 + (q & 3)];
             }
-            if (s == 256) break;
-            if (s > 285) return kInflateRetry;
-            const uint32_t le = ltab[s - 257];
-            const uint32_t len = (le & 0xffff) + in.bits(le >> 16);
-            in.refill();
-            const uint32_t ds = fixed ? __builtin_bitreverse32(in.peek(5)) >> 27 : dist.decode(in);
-            if (fixed) in.drop(5);
-            if (ds > 29) return kInflateRetry;
-            const uint32_t de = dtab[ds];
-            const uint32_t d = (de & 0xffff) + in.bits(de >> 16);
-            if (d > pos || pos + len > cap) return kInflateRetry;
-            lane_copy(out, pos, d, len, cap);
-            pos += len;
+            flushed = upto;
         }
-        if (in.bitpos() > (uint64_t)in.len * 8) return kInflateRetry;
-    } while (!bfinal);
-    const uint32_t t = (uint32_t)((in.bitpos() + 7) >> 3);
-    if (in.bitpos() > (uint64_t)in.len * 8 || t + 8 > in.len) return kInflateRetry;
-    const uint32_t isz = in.byte_at(t + 4) | in.byte_at(t + 5) << 8 | in.byte_at(t + 6) << 16 | in.byte_at(t + 7) << 24;
-    if (isz != pos) return kInflateRetry;
-    *crc_expect = in.byte_at(t) | in.byte_at(t + 1) << 8 | in.byte_at(t + 2) << 16 | in.byte_at(t + 3) << 24;
-    *out_len = pos;
-    return 0;
-}
+    }
+};
 
 __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lcol[];
     PMC_LDS uint16_t *col = to_lds<uint16_t>(lcol + threadIdx.x);
-    PMC_LDS uint32_t *ltab = to_lds<uint32_t>((uint8_t *)lcol + kLaneTabOff), *dtab = ltab + 32;
-    if (threadIdx.x < 29) ltab[threadIdx.x] = (uint32_t)c_lbase[threadIdx.x] | (uint32_t)c_lext[threadIdx.x] << 16;
-    if (threadIdx.x < 30) dtab[threadIdx.x] = (uint32_t)c_dbase[threadIdx.x] | (uint32_t)c_dext[threadIdx.x] << 16;
-    __syncthreads();
-    for (uint64_t v = (uint64_t)blockIdx.x * 64 + threadIdx.x; v < a.n; v += (uint64_t)gridDim.x * 64) {
-        const uint32_t in_len = a.src_len[v];
-        if (in_len == 0) {
+    PMC_LDS uint32_t *ring = to_lds<uint32_t>((uint8_t *)lcol + kLaneRingOff) + threadIdx.x;
+    PMC_LDS uint16_t *bcol = to_lds<uint16_t>((uint16_t *)((uint8_t *)lcol + kLaneRingOff) + threadIdx.x);
+    PMC_LDS uint32_t *winw = to_lds<uint32_t>((uint8_t *)lcol + kLaneWinOff) + threadIdx.x;
+    for (uint64_t vb = (uint64_t)blockIdx.x * 64; vb < a.n; vb += (uint64_t)gridDim.x * 64) {
+        const uint64_t v = vb + threadIdx.x;
+        const uint32_t in_len = v < a.n ? a.src_len[v] : 0u;
+        // st: 0 decoding, 1 end of block reached, 2 declined, 3 no member / empty input
+        uint32_t st = v < a.n ? 0u : 3u;
+        if (st == 0 && in_len == 0) {
             a.rc[v] = PMC_INVALID_INPUT_DEV;
             a.dst_len[v] = 0;
-            continue;
+            st = 3;
         }
         LaneIn in;
-        in.p = a.src + a.src_off[v];
+        in.p = st == 0 ? a.src + a.src_off[v] : a.src;
         in.len = in_len;
         in.blk = reinterpret_cast<const uint4 *>((uintptr_t)in.p & ~(uintptr_t)15);
-        uint32_t olen = 0, crc = 0;
-        const int rc = lane_inflate(in, a.dst + a.dst_off[v], a.dst_cap[v], col, ltab, dtab, &olen, &crc);
-        a.rc[v] = rc;
-        a.dst_len[v] = olen;
-        a.crc_expect[v] = crc;
+        LaneCode<15> lit, dist;
+        lit.base = (PMC_LDS int16_t *)(col + kColBaseL * 64);
+        lit.sym = col + kColLit * 64;
+        dist.base = (PMC_LDS int16_t *)(col + kColBaseD * 64);
+        dist.sym = col + kColDist * 64;
+        bool fixed = false;
+        if (st == 0 && !lane_prepare(in, col, bcol, lit, dist, fixed)) st = 2;
+        LaneWin win;
+        win.w = winw;
+        win.start(in, st == 0 ? in.bitpos() : 0);
+        const uint32_t cap = st == 0 ? a.dst_cap[v] : 0u;
+        LaneOut o;
+        o.dst = st == 0 ? a.dst + a.dst_off[v] : a.dst;
+        o.a0 = (uint32_t)((uintptr_t)o.dst & 3);
+        o.dw = reinterpret_cast<uint32_t *>((uintptr_t)o.dst & ~(uintptr_t)3);
+        o.rw = ring;
+        o.rb = (PMC_LDS uint8_t *)ring;
+        o.pos = 0;
+        o.flushed = 0;
+        uint32_t rem = 0, md = 0; // pending match: bytes left, distance
+        // one step per iteration: a symbol, then up to 8 bytes of the current match
+        while (ballot(st == 0)) {
+            if (ballot(st == 0 && win.needs()))
+                if (st == 0) win.advance();
+            if (st == 0) {
+                if (rem == 0) {
+                    win.refill();
+                    const uint32_t sy = fixed ? fixed_lit(win) : lit.decode(win);
+                    if (sy < 256) {
+                        if (o.pos >= cap) st = 2;
+                        else o.put(o.pos++, sy);
+                    } else if (sy == 256) {
+                        st = 1;
+                    } else if (sy > 285) {
+                        st = 2;
+                    } else {
+                        // length / distance bases and extra bits in closed form (RFC 1951 3.2.5)
+                        const uint32_t li = sy - 257;
+                        const uint32_t lx = li < 8 || li == 28 ? 0u : (li - 4) >> 2;
+                        const uint32_t lb = li < 8 ? li + 3 : li == 28 ? 258u : ((4 + (li & 3)) << lx) + 3;
+                        const uint32_t len = lb + win.bits(lx);
+                        win.refill();
+                        const uint32_t ds = fixed ? __builtin_bitreverse32(win.peek(5)) >> 27 : dist.decode(win);
+                        if (fixed) win.drop(5);
+                        const uint32_t dx = ds < 4 ? 0u : (ds >> 1) - 1;
+                        const uint32_t db = ds < 4 ? ds + 1 : ((2 + (ds & 1)) << dx) + 1;
+                        const uint32_t d = db + win.bits(dx < 14 ? dx : 0u);
+                        if (ds > 29 || d > o.pos || o.pos + len > cap) {
+                            st = 2;
+                        } else if (d < 8) { // period d: replicate it, later chunks copy from d' >= 8 back
+                            uint64_t pat = o.get8(o.pos - d, true) & ((1ull << (8 * d)) - 1);
+                            for (uint32_t w = d; w < 8; w <<= 1) pat |= pat << (8 * w);
+                            const uint32_t m = len < 8 ? len : 8;
+#pragma unroll
+                            for (uint32_t j = 0; j < 8; j++)
+                                if (j < m) o.put(o.pos + j, (uint32_t)(pat >> (8 * j)));
+                            o.pos += m;
+                            rem = len - m;
+                            md = d * ((8 + d - 1) / d);
+                        } else {
+                            rem = len;
+                            md = d;
+                        }
+                    }
+                }
+                if (st == 0 && rem) {
+                    const uint32_t m = rem < 8 ? rem : 8;
+                    const uint64_t x = o.get8(o.pos - md, md <= kRing - 16);
+#pragma unroll
+                    for (uint32_t j = 0; j < 8; j++)
+                        if (j < m) o.put(o.pos + j, (uint32_t)(x >> (8 * j)));
+                    o.pos += m;
+                    rem -= m;
+                }
+            }
+            // wave-synchronous flush: every lane writes its complete dwords at once, so the
+            // wave waits for stores a few times per member instead of once per lane flush
+            if (ballot(st == 0 && o.pos - o.flushed >= kFlush))
+                if (st == 0) o.flush(o.pos, false);
+        }
+        if (st == 1) {
+            if (win.bitpos() > (uint64_t)in.len * 8) st = 2;
+        }
+        if (st == 1) {
+            const uint32_t t = (uint32_t)((win.bitpos() + 7) >> 3);
+            if (t + 8 > in.len) {
+                st = 2;
+            } else {
+                const uint32_t isz = in.byte_at(t + 4) | in.byte_at(t + 5) << 8 | in.byte_at(t + 6) << 16 |
+                                     in.byte_at(t + 7) << 24;
+                if (isz != o.pos) {
+                    st = 2;
+                } else {
+                    o.flush(o.pos, true);
+                    a.crc_expect[v] =
+                        in.byte_at(t) | in.byte_at(t + 1) << 8 | in.byte_at(t + 2) << 16 | in.byte_at(t + 3) << 24;
+                    a.dst_len[v] = o.pos;
+                    a.rc[v] = 0;
+                }
+            }
+        }
+        if (st == 2) a.rc[v] = kInflateRetry;
     }
 }
 
