@@ -23,10 +23,9 @@
 
 namespace pmc {
 
-// chunk arrays: value v of a chunk is column v & 63 of block v >> 6
-__device__ __forceinline__ uint64_t col_index(uint64_t v, uint32_t row) {
-    return ((v >> 6) * kSplitRows + row) * 64 + (v & 63);
-}
+// Chunk arrays: histograms and code lengths are one contiguous row per value (the wave-
+// per-value kernels read and write them coalesced); the trees kernel's merge lists are
+// interleaved by 64-value block (lane-coalesced).
 
 // ---- front -------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256, 6) deflate_front_kernel(DeflateArgs a) {
@@ -58,7 +57,7 @@ __global__ void __launch_bounds__(256, 6) deflate_front_kernel(DeflateArgs a) {
             const uint32_t ntok = w.run_front(a.src + a.src_off[gv], len);
             // histograms -> column v of the chunk's interleaved u16 table
             for (int s = l; s < kLCodes + kDCodes; s += 64)
-                a.cH[col_index(v, (uint32_t)s)] = (uint16_t)(s < kLCodes ? w.lfreq[s] : w.dfreq[s - kLCodes]);
+                a.cH[v * kSplitRows + s] = (uint16_t)(s < kLCodes ? w.lfreq[s] : w.dfreq[s - kLCodes]);
             if (l == 0) a.cN[v] = ntok;
         }
     }
@@ -73,8 +72,8 @@ struct LaneTrees {
     PMC_LDS uint32_t *hp;  // heap, entry i at hp[i * 64]  (column of this lane)
     PMC_LDS uint16_t *blc; // bl_count[16]
     PMC_LDS uint16_t *blf; // bit-length tree frequencies [19]
-    const uint16_t *hist;  // global column: hist[sym * 64]
-    uint8_t *lens;         // global column: lens[sym * 64]
+    const uint16_t *hist;  // global, this value's row: hist[sym]
+    uint8_t *lens;         // global, this value's row: lens[sym]
     uint32_t *mg;          // global column: merge list, mg[i * 64]
     bool deferred = false;
 
@@ -103,7 +102,7 @@ struct LaneTrees {
     }
 
     // build_tree + gen_bitlen (trees.c) for one tree whose frequencies are freq(s), s < elems;
-    // leaf lengths go to lens[(row0 + s) * 64].  Returns max_code (-1 and `deferred` when the
+    // leaf lengths go to lens[row0 + s].  Returns max_code (-1 and `deferred` when the
     // heap would exceed CAP entries).
     template <class Freq>
     __device__ int build(Freq freq, int elems, uint32_t row0, const CtData *stree, const uint8_t *extra, int extra_base,
@@ -168,7 +167,7 @@ struct LaneTrees {
                 if (x >= (uint32_t)elems) {
                     setH(x - (uint32_t)elems + 1, bits);
                 } else {
-                    lens[(row0 + x) * 64] = (uint8_t)bits;
+                    lens[row0 + x] = (uint8_t)bits;
                     blc[bits * 64]++;
                     const uint32_t f = key >> 15;
                     const uint32_t xb = (int)x >= extra_base ? extra[x - extra_base] : 0u;
@@ -195,10 +194,10 @@ struct LaneTrees {
                     const uint32_t key = mg[idx * 64], x = key & 1023;
                     idx++;
                     if (x >= (uint32_t)elems) continue;
-                    const uint32_t cur = lens[(row0 + x) * 64];
+                    const uint32_t cur = lens[row0 + x];
                     if (cur != (uint32_t)bits) {
                         opt += ((int64_t)bits - (int64_t)cur) * (int64_t)(key >> 15);
-                        lens[(row0 + x) * 64] = (uint8_t)bits;
+                        lens[row0 + x] = (uint8_t)bits;
                     }
                     n--;
                 }
@@ -209,7 +208,7 @@ struct LaneTrees {
 
     // scan_tree (trees.c): bit-length tree frequencies for lengths lens[row0 .. row0 + max_code]
     __device__ void scan(uint32_t row0, int max_code) {
-        int prevlen = -1, nextlen = lens[row0 * 64], count = 0, max_count = 7, min_count = 4;
+        int prevlen = -1, nextlen = lens[row0], count = 0, max_count = 7, min_count = 4;
         if (nextlen == 0) max_count = 138, min_count = 3;
         int w0 = -8;
         uint64_t pk = 0; // lengths w0 .. w0 + 7, one byte each (fetched 8 at a time so the loads overlap)
@@ -221,7 +220,7 @@ struct LaneTrees {
                     pk = 0;
 #pragma unroll
                     for (int k = 0; k < 8; k++)
-                        pk |= (uint64_t)(w0 + k <= max_code ? lens[(row0 + w0 + k) * 64] : 0u) << (8 * k);
+                        pk |= (uint64_t)(w0 + k <= max_code ? lens[row0 + w0 + k] : 0u) << (8 * k);
                 }
                 nextlen = (int)((pk >> (8 * (nx - w0))) & 0xff);
             } else {
@@ -256,19 +255,19 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, PMC_LDS uint32_t *
     t.hp = col;
     t.blc = aux;
     t.blf = aux + 16 * 64;
-    t.hist = a.cH + col_index(v, 0);
-    t.lens = a.cL + col_index(v, 0);
+    t.hist = a.cH + v * kSplitRows;
+    t.lens = a.cL + v * kSplitRows;
     t.mg = a.cG + ((v >> 6) * kMergeRows) * 64 + (v & 63);
-    for (uint32_t s = 0; s < kSplitRows; s++) t.lens[s * 64] = 0;
+    for (uint32_t s = 0; s < kSplitRows; s += 16) *reinterpret_cast<uint4 *>(t.lens + s) = make_uint4(0, 0, 0, 0);
     int64_t opt = 0, stat = 0;
-    auto hist = [&](int s) -> uint32_t { return t.hist[s * 64]; };
+    auto hist = [&](int s) -> uint32_t { return t.hist[s]; };
     const int l_max = t.build(hist, kLCodes, 0, TT.static_ltree, TT.extra_lbits, kLiterals + 1, kMaxBits, opt, stat);
     if (t.deferred) {
         a.cP[v] = kPlanDeferred;
         a.cD[atomicAdd(a.cD + a.count, 1u)] = (uint32_t)v;
         return;
     }
-    auto dhist = [&](int s) -> uint32_t { return t.hist[(kLCodes + s) * 64]; };
+    auto dhist = [&](int s) -> uint32_t { return t.hist[kLCodes + s]; };
     const int d_max = t.build(dhist, kDCodes, kLCodes, TT.static_dtree, TT.extra_dbits, 0, kMaxBits, opt, stat);
     for (int s = 0; s < kBLCodes; s++) t.blf[s * 64] = 0;
     t.scan(0, l_max);
@@ -277,7 +276,7 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, PMC_LDS uint32_t *
     t.build(bfreq, kBLCodes, kLCodes + kDCodes, nullptr, TT.extra_blbits, 0, kMaxBLBits, opt, stat);
     int mbi;
     for (mbi = kBLCodes - 1; mbi >= 3; mbi--)
-        if (t.lens[(kLCodes + kDCodes + TT.bl_order[mbi]) * 64] != 0) break;
+        if (t.lens[kLCodes + kDCodes + TT.bl_order[mbi]] != 0) break;
     opt += 3 * ((int64_t)mbi + 1) + 5 + 5 + 4;
     uint32_t opt_lenb = (uint32_t)(((uint64_t)opt + 3 + 7) >> 3);
     const uint32_t static_lenb = (uint32_t)(((uint64_t)stat + 3 + 7) >> 3);
@@ -336,7 +335,7 @@ __global__ void __launch_bounds__(256, 4) deflate_back_kernel(DeflateArgs a) {
                 continue;
             }
             const uint32_t ntok = a.cN[v], plan = a.cP[v];
-            for (uint32_t s = l; s < kSplitRows; s += 64) Ls[s] = a.cL[col_index(v, s)];
+            for (uint32_t s = l; s < kSplitRows; s += 64) Ls[s] = a.cL[v * kSplitRows + s];
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
             const int rc = w.run_back(a.src + a.src_off[gv], len, ntok, plan, Ls, a.dst + a.dst_off[gv],
                                       a.dst_cap[gv], a.dst_len + gv);

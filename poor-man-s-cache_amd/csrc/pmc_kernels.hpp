@@ -42,8 +42,8 @@ struct DeflateArgs {
     uint64_t first, count;
     uint32_t *cT;  // LZ77 tokens, stride cap_len
     uint32_t *cN;  // token count per value
-    uint16_t *cH;  // symbol histograms, interleaved [block][kSplitRows][64]
-    uint8_t *cL;   // code lengths lit/len | dist | bit-length, interleaved [block][kSplitRows][64]
+    uint16_t *cH;  // symbol histograms, [value][kSplitRows]
+    uint8_t *cL;   // code lengths lit/len | dist | bit-length, [value][kSplitRows]
     uint32_t *cP;  // block plan per value
     uint32_t *cG;  // trees kernel merge lists, interleaved [block][kMergeRows][64]
     uint32_t *cD;  // values deferred to the large-heap trees pass; their number at cD[count]
