@@ -43,6 +43,12 @@ struct SmallLayout {
     uint64_t front_total, back_total; // split pipeline: front (stage..parse..histogram), back (emit)
 };
 
+// on-demand parse scratch from some offset o: CN u8[n] | HC u64[nw] | EV u32[64] + u8[64]
+__host__ __device__ inline uint64_t cn_hc_offset(uint64_t n) { return (n + 15) & ~(uint64_t)15; }
+__host__ __device__ inline uint64_t cn_ev_offset(uint64_t n) {
+    return cn_hc_offset(n) + ((((n + 63) / 64) * 8 + 15) & ~(uint64_t)15);
+}
+__host__ __device__ inline uint64_t cn_region_bytes(uint64_t n) { return cn_ev_offset(n) + 320; }
 __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
     auto a = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
     SmallLayout L;
@@ -83,7 +89,9 @@ __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
     L.M = L.X;
     L.masks = L.M + a(4 * n);
     L.masks_p = L.masks + a(((n + 63) / 64) * 8);
-    const uint64_t m = L.masks_p + a(((n + 63) / 64) * 8);
+    uint64_t m = L.masks_p + a(((n + 63) / 64) * 8);
+    const uint64_t mc = L.M + cn_region_bytes(n); // on-demand parse view (CN | HC | EV)
+    m = m > mc ? m : mc;
     uint64_t t = f > s ? f : s;
     t = t > m ? t : m;
     L.total = a(t);
@@ -104,7 +112,7 @@ __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
     F.S = a(n + 32);
     F.R = F.S + a(2 * n + 2);
     F.X = F.R + a(2 * n + 2);
-    const uint64_t xs = a(((n + 63) / 64) * 8) > 1024 ? a(((n + 63) / 64) * 8) : 1024;
+    const uint64_t xs = cn_region_bytes(n) > 1024 ? cn_region_bytes(n) : 1024;
     F.freq = F.S;
     const uint64_t t1 = F.X + xs, t2 = F.freq + 352 * 4;
     F.total = a(t1 > t2 ? t1 : t2);
@@ -241,9 +249,6 @@ struct TreeOut {
 };
 
 #define PMC_GLB __attribute__((address_space(1)))
-#ifndef PMC_GROUP
-#define PMC_GROUP 2
-#endif
 struct SmallWave {
     // every working array is LDS-typed (ds_* with 32-bit addresses)
     PMC_LDS uint8_t *b;
@@ -260,6 +265,8 @@ struct SmallWave {
     PMC_LDS uint16_t *T, *H, *cnt;
     PMC_LDS uint32_t *M;    // per-position match_all results (aliases the sort scratch)
     PMC_LDS uint64_t *HC;   // on-demand parse: bit x = position x has a chain candidate (aliases M)
+    PMC_LDS uint8_t *CN;    // on-demand parse: chain candidates of position x (capped at 255)
+    PMC_LDS uint32_t *EV;   // on-demand parse: eval scratch (64 best keys, then 64 u8 owner marks)
     PMC_LDS uint64_t *ML;   // segment walk: positions that start a match (or are unresolved)
     PMC_LDS uint64_t *MP;   // segment walk: positions where a lazy-improvement run ends
     PMC_GLB uint32_t *tok;
@@ -443,10 +450,7 @@ struct SmallWave {
     // parallel before the serial parse.  M[i] = best | bestq << 9 | (walk cut short) << 31
     // with best = max over those candidates of min(LCP, nice), bestq the nearest achieving
     // it.  A cut-short walk is finished by search() if the parse visits i.
-    // on-demand evaluation: kGroup positions per wave step, kPreCand = 64 / kGroup chain
-    // candidates per position (one lane each)
-    static constexpr uint32_t kGroup = PMC_GROUP;
-    static constexpr uint32_t kPreCand = 64 / kGroup;
+    static constexpr uint32_t kPreCand = 32;
     // Work-stealing walk, branch-light: every iteration each lane issues the same loads
     // (one chain entry, 8 bytes at i+off and at c+off, the two prune words) and advances
     // its state with selects -- a candidate is fetched, pruned, or compared 8 bytes further.
@@ -515,7 +519,7 @@ struct SmallWave {
     // Resumes a walk cut short by match_all: candidates kPreCand.. of position i, starting
     // from that walk's best / bestq.  Returns the match length (> b0) or 0; *q_out = the
     // nearest candidate achieving it.
-    __device__ uint32_t search(uint32_t i, uint32_t b0, uint32_t len, uint32_t best, uint32_t bestq,
+    __device__ __forceinline__ uint32_t search(uint32_t i, uint32_t b0, uint32_t len, uint32_t best, uint32_t bestq,
                                uint32_t *q_out) {
         const int l = lane_id();
         const uint32_t C = b0 >= 32 ? 1024u : 4096u;
@@ -683,80 +687,89 @@ struct SmallWave {
     // Only positions the lazy parse visits need longest_match (about 15 % of the positions of
     // a 1 KiB JSON value that have chain candidates at all).  The parse runs serially on the
     // scalar unit; whenever it reaches a position with candidates whose result is not at hand,
-    // one wave step evaluates that position and the next kGroup - 1 positions with candidates:
-    // each lane compares one (position, candidate) pair -- candidates 1..kPreCand of the chain,
-    // nearest first -- and a DPP row max picks (longest, then nearest).  A chain with more than
-    // kPreCand candidates is finished by search() when the parse uses it.  Positions without
-    // candidates (HC bit clear) are skipped in bulk as literals.
-    __device__ void build_hc(uint32_t npos) {
+    // one wave step evaluates that position and the following ones, each taking as many lanes
+    // as it has chain candidates (capped at kPreCand, nearest first) until the 64 lanes are
+    // used: each lane compares one (position, candidate) pair and an LDS max per position picks
+    // (longest, then nearest).  A chain with more than kPreCand candidates is finished by
+    // search() when the parse uses it.  Positions without candidates (CN = 0, HC bit clear)
+    // are skipped in bulk as literals.
+    // CN[x] = chain candidates of x = entries before x in its run of the hash-sorted order,
+    // less position 0 (zlib's NIL: head[] value 0 never starts a match; the sort is stable,
+    // so position 0 is the first entry of its run).  HC = CN > 0 as bits.
+    __device__ __forceinline__ void build_cn(uint32_t npos) {
         const uint32_t l = (uint32_t)lane_id();
+        const uint32_t k0 = rfl((uint32_t)R[0]);
+        uint32_t ph = 0xffffffffu, prs = 0; // previous chunk's last hash and run start
+        for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+            const uint32_t k = c0 + l;
+            const bool valid = k < npos;
+            const uint32_t p = valid ? (uint32_t)S[k] : 0u;
+            const uint32_t h = valid ? hash3(load4(p)) : 0xfffffffeu;
+            uint32_t hp = (uint32_t)__shfl_up((int)h, 1);
+            hp = l == 0 ? ph : hp;
+            uint32_t rs = wave_incl_max_dpp(valid && h != hp ? k : 0u);
+            rs = rs > prs ? rs : prs;
+            const uint32_t cnt = k - rs - (rs == k0 && k > rs ? 1u : 0u);
+            if (valid) CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
+            ph = readlane(h, 63);
+            prs = readlane(rs, 63);
+        }
+        wave_sync();
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
             const uint32_t x = c0 + l;
-            bool v = x < npos;
-            const uint32_t r = v ? R[x] : 0u;
-            v = v && r >= 1;
-            const uint32_t q = v ? S[r - 1] : 0u;
-            v = v && q != 0 && hash3(load4(q)) == hash3(load4(x));
-            const uint64_t m = ballot(v);
+            const uint64_t m = ballot(x < npos && CN[x] != 0);
             if (l == 0) HC[c0 >> 6] = m;
         }
         wave_sync();
     }
-    // results of the current group: position (or ~0) and best | q << 9 | cut << 31
+    // results of the current eval: window start p0, evaluated offsets m (uniform) and, in
+    // lane j, best | q << 9 | cut << 31 for position p0 + j
     struct Group {
-        uint32_t p[kGroup], e[kGroup];
+        uint32_t p0;
+        uint64_t m;
+        uint32_t e;
     };
     __device__ void eval_group(Group &g, uint32_t p0, uint32_t npos, uint32_t len) {
-        const uint32_t l = (uint32_t)lane_id(), nw = (npos + 63) >> 6;
-        g.p[0] = p0;
-#pragma unroll
-        for (uint32_t r = 1; r < kGroup; r++)
-            g.p[r] = g.p[r - 1] == 0xffffffffu ? 0xffffffffu : ffs_mask(HC, g.p[r - 1] + 1, nw);
-        const uint32_t row = l / kPreCand, d = l % kPreCand + 1;
-        uint32_t P = g.p[0];
-#pragma unroll
-        for (uint32_t r = 1; r < kGroup; r++) P = row == r ? g.p[r] : P;
-        bool v = P != 0xffffffffu;
-        P = v ? P : 0u;
-        const int k = v ? (int)R[P] - (int)d : -1;
-        v = k >= 0;
-        const uint32_t q = v ? S[k] : 0u;
-        v = v && q != 0;
+        const uint32_t l = (uint32_t)lane_id();
+        const uint32_t x = p0 + l;
+        const uint32_t cn = x < npos ? (uint32_t)CN[x] : 0u;
+        const uint32_t w = cn < kPreCand ? cn : kPreCand;
+        const uint32_t incl = wave_incl_scan_dpp(w), offs = incl - w;
+        const bool inc = w != 0 && incl <= 64;
+        const uint64_t im = ballot(inc); // a prefix of the window's has-candidate offsets
+        const uint32_t nl = readlane(incl, 63 - __builtin_clzll(im));
+        // lane -> owning offset: mark each evaluated offset's first lane, then max-scan
+        PMC_LDS uint8_t *mk = (PMC_LDS uint8_t *)(EV + 64);
+        EV[l] = 0;
+        mk[l] = 0;
+        if (inc) mk[offs] = (uint8_t)(l + 1);
+        wave_sync();
+        const bool v = l < nl;
+        const uint32_t own = v ? wave_incl_max_dpp(mk[l]) - 1 : 0u;
+        const uint32_t oo = (uint32_t)__shfl((int)offs, (int)own);
+        const uint32_t P = p0 + own, d = l - oo + 1;
+        const uint32_t q = v ? (uint32_t)S[(uint32_t)R[P] - d] : 0u;
         const uint64_t A = load8(P), B = load8(q);
-        v = v && hash3((uint32_t)A) == hash3((uint32_t)B);
         const uint32_t nice = (len - P) < 258 ? (len - P) : 258;
         const uint64_t y = A ^ B;
         uint32_t cl = y ? (uint32_t)__builtin_ctzll(y) >> 3 : 8u;
         bool ext = v && y == 0 && nice > 8;
         uint32_t off = 8;
         while (ballot(ext)) {
-            count(13);
             const uint64_t y2 = load8(ext ? P + off : 0u) ^ load8(ext ? q + off : 0u);
             cl = ext ? (y2 ? off + ((uint32_t)__builtin_ctzll(y2) >> 3) : off + 8) : cl;
             ext = ext && y2 == 0 && off + 8 < nice;
             off += 8;
         }
         cl = cl < nice ? cl : nice;
-        uint32_t key = v ? (cl << 23 | (kPreCand - d) << 18 | q) : 0u;
-        key = dpp_row_max(key);
-        const uint64_t vm = ballot(v);
-        uint32_t rk[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) rk[r] = readlane(key, 16 * r);
-#pragma unroll
-        for (uint32_t r = 0; r < kGroup; r++) {
-            uint32_t kk = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 4 / kGroup; j++) {
-                const uint32_t x = rk[r * (4 / kGroup) + j];
-                kk = x > kk ? x : kk;
-            }
-            const uint64_t rowm = (vm >> (r * kPreCand)) & (kPreCand == 64 ? ~0ull : ((1ull << kPreCand) - 1));
-            const uint32_t best = kk >> 23, pr = g.p[r];
-            const uint32_t nice_r = (len - pr) < 258 ? (len - pr) : 258;
-            const bool full = rowm == (kPreCand == 64 ? ~0ull : ((1ull << kPreCand) - 1));
-            g.e[r] = best | (kk & 0x3fffu) << 9 | ((full && best < nice_r) ? 1u << 31 : 0u);
-        }
+        if (v) __hip_atomic_fetch_max(&EV[own], cl << 23 | (kPreCand - d) << 18 | q, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WAVEFRONT);
+        wave_sync();
+        const uint32_t kk = EV[l], best = kk >> 23;
+        const uint32_t nx = (len - x) < 258 ? (len - x) : 258;
+        g.p0 = p0;
+        g.m = im;
+        g.e = best | (kk & 0x3fffu) << 9 | (cn > kPreCand && best < nx ? 1u << 31 : 0u);
     }
     // Token sink: tokens collect in one VGPR (lane k holds token 64 * block + k) and leave
     // with one coalesced store per 64 tokens, so emitting costs no exec-masked stores.
@@ -785,29 +798,35 @@ struct SmallWave {
         const uint32_t l = (uint32_t)lane_id();
         if (l < (t.n & 63)) tok[(t.n & ~63u) + l] = t.v;
     }
-    // longest_match record of has-candidate position x (evaluating a new group if needed)
+    // longest_match record of has-candidate position x (evaluating a new window if needed)
     __device__ uint32_t group_get(Group &g, uint32_t x, uint32_t npos, uint32_t len) {
-        uint32_t e = 0xffffffffu;
-#pragma unroll
-        for (uint32_t r = 0; r < kGroup; r++) e = g.p[r] == x ? g.e[r] : e;
-        if (e == 0xffffffffu) {
-            eval_group(g, x, npos, len);
-#pragma unroll
-            for (uint32_t r = 0; r < kGroup; r++) {
-                g.p[r] = rfl(g.p[r]);
-                g.e[r] = rfl(g.e[r]);
-            }
-            e = g.e[0];
-        }
-        return e;
+        const uint32_t off = x - g.p0;
+        if (off < 64 && ((g.m >> off) & 1)) return readlane(g.e, (int)off);
+        stamp(2);
+        eval_group(g, x, npos, len);
+        stamp(10);
+        count(13);
+        return readlane(g.e, 0);
     }
+    // (a noinline member reaches the wave state through `this`, a pointer to scratch: every
+    // member pointer would be re-read from memory inside the loop.  A local copy lives in SGPRs.)
     __device__ __noinline__ uint32_t parse_ondemand(uint32_t npos_, uint32_t len_) {
+        SmallWave me = *this;
+        const uint32_t r = me.parse_ondemand_body(npos_, len_);
+#ifdef PMC_STAMPS
+        for (int k = 0; k < 16; k++) st[k] = me.st[k];
+        t_last = me.t_last;
+#endif
+        return r;
+    }
+    __device__ __forceinline__ uint32_t parse_ondemand_body(uint32_t npos_, uint32_t len_) {
         const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
         const uint32_t nw = (npos + 63) >> 6;
-        build_hc(npos);
+        build_cn(npos);
         Group g;
-#pragma unroll
-        for (uint32_t r = 0; r < kGroup; r++) g.p[r] = 0xffffffffu;
+        g.p0 = 0xffffffffu;
+        g.m = 0;
+        g.e = 0;
         TokBuf tb;
         uint32_t i = 0, ml = 2, ms = 0, av = 0;
         uint32_t hci = 0;              // HC word cached in SGPRs
@@ -1561,7 +1580,7 @@ struct SmallWave {
         const uint32_t npos = len >= 3 ? len - 2 : 0;
         uint32_t ntok;
         if (npos) {
-            sort_positions2(npos, (PMC_LDS uint32_t *)HC);
+            sort_positions2(npos, (PMC_LDS uint32_t *)CN);
             stamp(1);
             ntok = parse_ondemand(npos, len);
         } else {
@@ -1707,7 +1726,9 @@ __device__ inline void small_wave_init(SmallWave &w, uint8_t *base, const SmallL
     w.H = w.R; // hash keys live in R until the ranks overwrite them
     w.cnt = to_lds<uint16_t>(base + L.cnt);
     w.M = to_lds<uint32_t>(base + L.M);
-    w.HC = to_lds<uint64_t>(base + L.M);
+    w.CN = to_lds<uint8_t>(base + L.M);
+    w.HC = to_lds<uint64_t>(base + L.M + cn_hc_offset(a.cap_len));
+    w.EV = to_lds<uint32_t>(base + L.M + cn_ev_offset(a.cap_len));
     w.crc_tab = to_lds<const uint32_t>((void *)crc_tab);
     for (int k = 0; k < 16; k++) w.st[k] = 0;
     w.stop = a.stop_after;
@@ -1754,7 +1775,9 @@ __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
     w.H = w.R; // hash keys live in R until the ranks overwrite them
     w.cnt = to_lds<uint16_t>(base + L.cnt);
     w.M = to_lds<uint32_t>(base + L.M);
-    w.HC = to_lds<uint64_t>(base + L.M);
+    w.CN = to_lds<uint8_t>(base + L.M);
+    w.HC = to_lds<uint64_t>(base + L.M + cn_hc_offset(a.cap_len));
+    w.EV = to_lds<uint32_t>(base + L.M + cn_ev_offset(a.cap_len));
     w.ML = to_lds<uint64_t>(base + L.masks);
     w.MP = to_lds<uint64_t>(base + L.masks_p);
     w.tok = (PMC_GLB uint32_t *)(a.tokens + wave * kSlabSyms);

@@ -40,7 +40,9 @@ __global__ void __launch_bounds__(256, 6) deflate_front_kernel(DeflateArgs a) {
     small_wave_init(w, base, L, a, nullptr);
     w.S = to_lds<uint16_t>(base + F.S);
     w.R = to_lds<uint16_t>(base + F.R);
-    w.HC = to_lds<uint64_t>(base + F.X);
+    w.CN = to_lds<uint8_t>(base + F.X);
+    w.HC = to_lds<uint64_t>(base + F.X + cn_hc_offset(a.cap_len));
+    w.EV = to_lds<uint32_t>(base + F.X + cn_ev_offset(a.cap_len));
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;

@@ -108,6 +108,24 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
     return v;
 }
+// inclusive max-scan over the wave (same DPP pattern; lanes shifted in read 0, the identity
+// for unsigned max)
+__device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t v) {
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v = t > v ? t : v;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    v = t > v ? t : v;
+    return v;
+}
 // row-level butterfly with quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror:
 // afterwards every lane holds the max of its 16-lane row.
 __device__ __forceinline__ uint32_t dpp_row_max(uint32_t v) {
