@@ -358,6 +358,10 @@ struct SmallWave {
     // the same digit comes from one ballot per digit bit (match mask + mbcnt), so the scatter
     // is stable without per-lane counters.
     __device__ __noinline__ void sort_positions2(uint32_t npos_, PMC_LDS uint32_t *tab) {
+        SmallWave me = *this; // (see parse_ondemand)
+        me.sort_positions2_body(npos_, tab);
+    }
+    __device__ __forceinline__ void sort_positions2_body(uint32_t npos_, PMC_LDS uint32_t *tab) {
         const uint32_t npos = rfl(npos_);
         const uint32_t l = (uint32_t)lane_id();
         PMC_LDS uint16_t *Tt = R;

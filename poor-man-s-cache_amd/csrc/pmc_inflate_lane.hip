@@ -38,10 +38,17 @@ constexpr uint32_t kLaneRingOff = (kLaneTabOff + 64 * 4 + 255) & ~255u;    // ou
 constexpr uint32_t kLaneWinOff = kLaneRingOff + 256 / 4 * 64 * 4;          // input windows (LaneWin)
 constexpr uint32_t kLaneLdsBytes = kLaneWinOff + 32 * 64 * 4;
 
+// 16-byte load through a global (not flat) pointer: flat loads also count against lgkmcnt,
+// so every LDS wait would wait for them too
+__device__ __forceinline__ uint4 gload16(PMC_GLB const uint4 *p) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u v = *(PMC_GLB const v4u *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 struct LaneIn {
     const uint8_t *p;
     uint32_t len;       // member bytes
-    const uint4 *blk;   // aligned block base (p rounded down to 16)
+    PMC_GLB const uint4 *blk; // aligned block base (p rounded down to 16); global, not flat
     uint32_t bi;        // index of the block in `cur`
     uint4 cur, nxt;     // block bi and bi + 1
     uint32_t wi;        // next dword of `cur` to move into buf
@@ -51,7 +58,7 @@ struct LaneIn {
     __device__ uint32_t byte_at(uint32_t i) const { return i < len ? (uint32_t)p[i] : 0u; }
     // block k of the stream, or zeros past the member's last block (never touches its page)
     __device__ uint4 block(uint32_t k) const {
-        return (uint64_t)k * 16 < ((uintptr_t)p & 15) + (uint64_t)len ? blk[k] : make_uint4(0, 0, 0, 0);
+        return (uint64_t)k * 16 < ((uintptr_t)p & 15) + (uint64_t)len ? gload16(blk + k) : make_uint4(0, 0, 0, 0);
     }
     __device__ void refill() {
         if (n <= 32) {
@@ -101,14 +108,14 @@ struct LaneIn {
 // loads a few times per member instead of whenever any one lane's buffer runs low.
 struct LaneWin {
     PMC_LDS uint32_t *w; // slot s at w[s * 64]
-    const uint4 *blk;    // member rounded down to 16 bytes
+    PMC_GLB const uint4 *blk; // member rounded down to 16 bytes
     uint32_t nblk;       // blocks holding member bytes
     uint32_t head;       // member start - blk, in bits
     uint32_t wlo;        // first dword held
     uint32_t nd;         // next dword to move into buf
     uint64_t buf;
     uint32_t n;
-    __device__ uint4 block(uint32_t k) const { return k < nblk ? blk[k] : make_uint4(0, 0, 0, 0); }
+    __device__ uint4 block(uint32_t k) const { return k < nblk ? gload16(blk + k) : make_uint4(0, 0, 0, 0); }
     __device__ void load16(uint32_t d0) { // dwords d0 .. d0 + 15 (d0 % 16 == 0) into their slots
 #pragma unroll
         for (int b = 0; b < 4; b++) {
@@ -346,8 +353,8 @@ constexpr uint32_t kRing = 256, kFlush = 128;
 struct LaneOut {
     PMC_LDS uint8_t *rb;  // byte view of the lane's ring column (byte q at (q >> 2) * 256 + (q & 3))
     PMC_LDS uint32_t *rw; // dword view (dword k at k * 64)
-    uint32_t *dw;         // dst rounded down to 4 bytes
-    uint8_t *dst;
+    PMC_GLB uint32_t *dw; // dst rounded down to 4 bytes (global, not flat: see gload16)
+    PMC_GLB uint8_t *dst;
     uint32_t a0;          // dst & 3
     uint32_t pos, flushed; // bytes produced / bytes in dst
     __device__ void put(uint32_t p, uint32_t b) {
@@ -409,7 +416,7 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
         LaneIn in;
         in.p = st == 0 ? a.src + a.src_off[v] : a.src;
         in.len = in_len;
-        in.blk = reinterpret_cast<const uint4 *>((uintptr_t)in.p & ~(uintptr_t)15);
+        in.blk = (PMC_GLB const uint4 *)((uintptr_t)in.p & ~(uintptr_t)15);
         LaneCode<15> lit, dist;
         lit.base = (PMC_LDS int16_t *)(col + kColBaseL * 64);
         lit.sym = col + kColLit * 64;
@@ -422,9 +429,9 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
         win.start(in, st == 0 ? in.bitpos() : 0);
         const uint32_t cap = st == 0 ? a.dst_cap[v] : 0u;
         LaneOut o;
-        o.dst = st == 0 ? a.dst + a.dst_off[v] : a.dst;
+        o.dst = (PMC_GLB uint8_t *)(st == 0 ? a.dst + a.dst_off[v] : a.dst);
         o.a0 = (uint32_t)((uintptr_t)o.dst & 3);
-        o.dw = reinterpret_cast<uint32_t *>((uintptr_t)o.dst & ~(uintptr_t)3);
+        o.dw = (PMC_GLB uint32_t *)((uintptr_t)o.dst & ~(uintptr_t)3);
         o.rw = ring;
         o.rb = (PMC_LDS uint8_t *)ring;
         o.pos = 0;
