@@ -44,6 +44,7 @@ struct SmallLayout {
 };
 
 // on-demand parse scratch from some offset o: CN u8[n] | HC u64[nw] | EV u32[64] + u8[64]
+// (320 B: at 1 KiB one more byte per wave costs a block of 4 waves per CU)
 __host__ __device__ inline uint64_t cn_hc_offset(uint64_t n) { return (n + 15) & ~(uint64_t)15; }
 __host__ __device__ inline uint64_t cn_ev_offset(uint64_t n) {
     return cn_hc_offset(n) + ((((n + 63) / 64) * 8 + 15) & ~(uint64_t)15);
@@ -266,7 +267,7 @@ struct SmallWave {
     PMC_LDS uint32_t *M;    // per-position match_all results (aliases the sort scratch)
     PMC_LDS uint64_t *HC;   // on-demand parse: bit x = position x has a chain candidate (aliases M)
     PMC_LDS uint8_t *CN;    // on-demand parse: chain candidates of position x (capped at 255)
-    PMC_LDS uint32_t *EV;   // on-demand parse: eval scratch (64 best keys, then 64 u8 owner marks)
+    PMC_LDS uint32_t *EV;   // on-demand parse: eval scratch (64 best keys, 64 u8 owner marks)
     PMC_LDS uint64_t *ML;   // segment walk: positions that start a match (or are unresolved)
     PMC_LDS uint64_t *MP;   // segment walk: positions where a lazy-improvement run ends
     PMC_GLB uint32_t *tok;
@@ -288,7 +289,7 @@ struct SmallWave {
         st[k]++;
 #endif
     }
-#ifdef PMC_STAMPS
+#if defined(PMC_STAMPS) || defined(PMC_PHASE_STOP)
 #define PMC_STOP(k, ret)                                                                                               \
     if (stop == (k)) return ret;
 #else
@@ -422,6 +423,10 @@ struct SmallWave {
         const uint32_t w = p >> 2, sh = p & 3;
         const uint32_t w0 = bw[w], w1 = bw[w + 1], w2 = bw[w + 2];
         return (uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32 | __builtin_amdgcn_alignbyte(w1, w0, sh);
+    }
+    // leading equal bytes of two 8-byte words given their xor y (8 when equal), branch-free
+    __device__ static uint32_t eq_bytes8(uint64_t y) {
+        return ((uint32_t)__builtin_ctzll(y | (1ull << 63)) >> 3) + (y == 0 ? 1u : 0u);
     }
     // common prefix of positions i and q (first words wi, wq already loaded), capped at nice
     __device__ uint32_t lcp(uint32_t i, uint32_t q, uint32_t wi, uint32_t wq, uint32_t nice) const {
@@ -732,48 +737,92 @@ struct SmallWave {
         uint32_t p0;
         uint64_t m;
         uint32_t e;
+        uint64_t stop; // offsets where a fresh-state walk stops: usable or cut, or not evaluated
+        uint64_t fast; // evaluated, usable, not cut, and position + 1 does not improve on it
+        uint64_t impr; // evaluated, usable, not cut, < 258, and position + 1 improves on it
+        uint64_t cut;  // evaluated, walk cut short (search() decides)
     };
+    // 16 bytes at p as two 8-byte words (5 dword reads + alignbyte)
+    __device__ void load16(uint32_t p, uint64_t &lo, uint64_t &hi) const {
+        const uint32_t w = p >> 2, sh = p & 3;
+        const uint32_t w0 = bw[w], w1 = bw[w + 1], w2 = bw[w + 2], w3 = bw[w + 3], w4 = bw[w + 4];
+        lo = (uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32 | __builtin_amdgcn_alignbyte(w1, w0, sh);
+        hi = (uint64_t)__builtin_amdgcn_alignbyte(w4, w3, sh) << 32 | __builtin_amdgcn_alignbyte(w3, w2, sh);
+    }
+    // The eval is a chain of dependent LDS round trips (the wave waits on each), so it is laid
+    // out to need few: (1) CN, CN + 1 and R of the window's positions; (2) each evaluated
+    // position's first lane receives (offset, position, R) through one store + load, spread to
+    // its other lanes by a max-scan; (3) the candidate S[R - d] and 16 bytes at the position;
+    // (4) 16 bytes at the candidate; then 16 bytes per step while some lane still matches;
+    // (5) an LDS max per position and its read-back.  Lanes outside the evaluated prefix
+    // compute on clamped indices and contribute key 0 (no exec-mask branches).
     __device__ void eval_group(Group &g, uint32_t p0, uint32_t npos, uint32_t len) {
         const uint32_t l = (uint32_t)lane_id();
         const uint32_t x = p0 + l;
-        const uint32_t cn = x < npos ? (uint32_t)CN[x] : 0u;
+        const uint32_t xc = x < npos ? x : 0u;
+        uint32_t cn = CN[xc], cn1 = CN[x + 1 < npos ? x + 1 : 0u];
+        const uint32_t rx = R[xc];
+        cn = x < npos ? cn : 0u;
+        cn1 = x + 1 < npos ? cn1 : 0u;
         const uint32_t w = cn < kPreCand ? cn : kPreCand;
         const uint32_t incl = wave_incl_scan_dpp(w), offs = incl - w;
         const bool inc = w != 0 && incl <= 64;
         const uint64_t im = ballot(inc); // a prefix of the window's has-candidate offsets
         const uint32_t nl = readlane(incl, 63 - __builtin_clzll(im));
-        // lane -> owning offset: mark each evaluated offset's first lane, then max-scan
-        PMC_LDS uint8_t *mk = (PMC_LDS uint8_t *)(EV + 64);
+        // first lane of each evaluated offset j: offs << 26 | (j + 1) << 19 | R (offs grows
+        // with j, so a max-scan hands every lane its owner); other lanes store to dummy slots
+        PMC_LDS uint32_t *dmy = EV + 64; // (the u8 mark area, 16 words)
         EV[l] = 0;
-        mk[l] = 0;
-        if (inc) mk[offs] = (uint8_t)(l + 1);
+        (inc ? EV : dmy)[inc ? offs : (l & 15)] = offs << 26 | (l + 1) << 19 | rx;
         wave_sync();
+        const uint32_t mk = EV[l];
+        EV[l] = 0; // (LDS keeps one wave's accesses in order: the read above sees the marks)
         const bool v = l < nl;
-        const uint32_t own = v ? wave_incl_max_dpp(mk[l]) - 1 : 0u;
-        const uint32_t oo = (uint32_t)__shfl((int)offs, (int)own);
-        const uint32_t P = p0 + own, d = l - oo + 1;
-        const uint32_t q = v ? (uint32_t)S[(uint32_t)R[P] - d] : 0u;
-        const uint64_t A = load8(P), B = load8(q);
+        const uint32_t sc = wave_incl_max_dpp(mk);
+        const uint32_t own = v ? ((sc >> 19) & 127) - 1 : 0u;
+        const uint32_t P = p0 + own, d = l - (sc >> 26) + 1;
+        uint32_t q = S[v ? (sc & 0x7ffffu) - d : 0u];
+        uint64_t A0, A1, B0, B1;
+        load16(P, A0, A1);
+        q = v ? q : 0u;
+        load16(q, B0, B1);
         const uint32_t nice = (len - P) < 258 ? (len - P) : 258;
-        const uint64_t y = A ^ B;
-        uint32_t cl = y ? (uint32_t)__builtin_ctzll(y) >> 3 : 8u;
-        bool ext = v && y == 0 && nice > 8;
-        uint32_t off = 8;
+        const uint64_t y0 = A0 ^ B0, y1 = A1 ^ B1;
+        uint32_t cl = y0 ? eq_bytes8(y0) : 8u + eq_bytes8(y1);
+        bool ext = v && (y0 | y1) == 0 && nice > 16;
+        uint32_t off = 16;
         while (ballot(ext)) {
-            const uint64_t y2 = load8(ext ? P + off : 0u) ^ load8(ext ? q + off : 0u);
-            cl = ext ? (y2 ? off + ((uint32_t)__builtin_ctzll(y2) >> 3) : off + 8) : cl;
-            ext = ext && y2 == 0 && off + 8 < nice;
-            off += 8;
+            count(8);
+            uint64_t C0, C1, D0, D1;
+            load16(ext ? P + off : 0u, C0, C1);
+            load16(ext ? q + off : 0u, D0, D1);
+            const uint64_t z0 = C0 ^ D0, z1 = C1 ^ D1;
+            cl = ext ? off + (z0 ? eq_bytes8(z0) : 8u + eq_bytes8(z1)) : cl;
+            ext = ext && (z0 | z1) == 0 && off + 16 < nice;
+            off += 16;
         }
         cl = cl < nice ? cl : nice;
-        if (v) __hip_atomic_fetch_max(&EV[own], cl << 23 | (kPreCand - d) << 18 | q, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_max(&EV[own], v ? cl << 23 | (kPreCand - d) << 18 | q : 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WAVEFRONT);
         wave_sync();
         const uint32_t kk = EV[l], best = kk >> 23;
         const uint32_t nx = (len - x) < 258 ? (len - x) : 258;
+        const bool cut = cn > kPreCand && best < nx;
+        const uint32_t bq = kk & 0x3fffu, e = best | bq << 9 | (cut ? 1u << 31 : 0u);
         g.p0 = p0;
         g.m = im;
-        g.e = best | (kk & 0x3fffu) << 9 | (cn > kPreCand && best < nx ? 1u << 31 : 0u);
+        g.e = e;
+        // walk masks (the fast path of deflate_slow, per offset); e of offset l + 1 via DPP
+        const bool ev = (im >> l) & 1;
+        const bool usable = best >= 4 || (best == 3 && x - bq <= 4096); // TOO_FAR
+        const uint32_t en = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x130, 0xf, 0xf, false); // wave_shl:1
+        const bool ev1 = l < 63 && ((im >> (l + 1)) & 1);
+        const bool no_impr = best >= 258 || cn1 == 0 || (ev1 && !(en >> 31) && (en & 511) <= best);
+        const bool impr = best < 258 && ev1 && !(en >> 31) && (en & 511) > best;
+        g.stop = ballot(ev ? (usable || cut) : cn != 0);
+        g.fast = ballot(ev && usable && !cut && no_impr);
+        g.impr = ballot(ev && usable && !cut && impr);
+        g.cut = ballot(ev && cut);
     }
     // Token sink: tokens collect in one VGPR (lane k holds token 64 * block + k) and leave
     // with one coalesced store per 64 tokens, so emitting costs no exec-masked stores.
@@ -790,6 +839,7 @@ struct SmallWave {
     __device__ void tb_run(TokBuf &t, uint32_t p, uint32_t cnt) {
         const uint32_t l = (uint32_t)lane_id();
         while (cnt) {
+            count(7);
             const uint32_t o = t.n & 63, take = cnt < 64 - o ? cnt : 64 - o;
             t.v = l - o < take ? p + (l - o) : t.v;
             t.n += take;
@@ -827,9 +877,11 @@ struct SmallWave {
         const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
         const uint32_t nw = (npos + 63) >> 6;
         build_cn(npos);
+        stamp(11);
+        PMC_STOP(13, 0)
         Group g;
         g.p0 = 0xffffffffu;
-        g.m = 0;
+        g.m = g.stop = g.fast = g.impr = g.cut = 0;
         g.e = 0;
         TokBuf tb;
         uint32_t i = 0, ml = 2, ms = 0, av = 0;
@@ -842,6 +894,7 @@ struct SmallWave {
             ms = rfl(ms);
             av = rfl(av);
             tb.n = rfl(tb.n);
+            count(14);
             if (ml == 2) {
                 // no pending match: positions without chain candidates only pass the pending
                 // literal on, so jump to the next position that has candidates
@@ -867,42 +920,61 @@ struct SmallWave {
                     i = j;
                     if (i >= len) break;
                 }
-                // fast path at a has-candidate position i with no pending match (i < npos):
-                // an unusable result is a literal step; a usable one that position i + 1 does
-                // not improve on is emitted at once.  Cut walks and lazy improvements take the
-                // general step below.
-                if (i < npos) {
-                    const uint32_t e0 = group_get(g, i, npos, len);
-                    if (!(e0 >> 31)) {
-                        const uint32_t b0 = e0 & 511, q0 = (e0 >> 9) & 0x3fffu;
-                        if (!(b0 >= 4 || (b0 == 3 && i - q0 <= 4096))) {
-                            if (av) tb_put(tb, i - 1);
-                            av = 1;
-                            i++;
-                            continue;
-                        }
-                        bool lazy = false;
-                        const uint32_t x = i + 1;
-                        if (b0 < 258 && x < npos) {
-                            if ((x >> 6) != hci) {
-                                hci = x >> 6;
-                                hcw = rfl64(HC[hci]);
-                            }
-                            if ((hcw >> (x & 63)) & 1) {
-                                const uint32_t e1 = group_get(g, x, npos, len);
-                                lazy = (e1 >> 31) || (e1 & 511) > b0;
-                            }
-                        }
-                        if (!lazy) {
-                            if (av) tb_put(tb, i - 1);
-                            tb_put(tb, ((i - q0) << 16) | (b0 - 3));
-                            i += b0;
-                            av = 0;
-                            continue;
-                        }
+                // Window walk from a fresh state at has-candidate position i (< npos): in the
+                // evaluated window, unusable results pass as literals and a usable one that
+                // position + 1 does not improve on is emitted at once (eval_group's stop / fast
+                // masks), so one step covers a literal run and its match.  Cut walks and lazy
+                // improvements take the general step below; an unevaluated position with
+                // candidates starts a new window.
+                uint32_t off = i - g.p0;
+                if (!(off < 64 && ((g.m >> off) & 1))) {
+                    stamp(2);
+                    eval_group(g, i, npos, len);
+                    stamp(10);
+                    count(13);
+                    off = 0;
+                }
+                const uint64_t sm = g.stop >> off;
+                if (!sm) { // literals to the window's end
+                    const uint32_t to = g.p0 + 64 < len ? g.p0 + 64 : len;
+                    const uint32_t from = av ? i - 1 : i;
+                    tb_run(tb, from, to - 1 - from);
+                    av = 1;
+                    i = to;
+                    continue;
+                }
+                const uint32_t sj = off + (uint32_t)__builtin_ctzll(sm), js = g.p0 + sj;
+                if (js > i) {
+                    const uint32_t from = av ? i - 1 : i;
+                    tb_run(tb, from, js - 1 - from);
+                    av = 1;
+                    i = js;
+                    if (!((g.m >> sj) & 1)) continue; // unevaluated: new window at js
+                }
+                if (!((g.cut >> sj) & 1)) {
+                    // usable at js: the run of lazy improvements js, js + 1, ... ends at t (bit
+                    // 63 of impr is always clear); positions js .. t - 1 become literals
+                    const uint32_t st = sj + (uint32_t)__builtin_ctzll(~(g.impr >> sj)), t = g.p0 + st;
+                    const uint32_t e0 = readlane(g.e, (int)st);
+                    const uint32_t b0 = e0 & 511, q0 = (e0 >> 9) & 0x3fffu;
+                    if (av) tb_put(tb, i - 1);
+                    tb_run(tb, i, t - i);
+                    if ((g.fast >> st) & 1) {
+                        tb_put(tb, ((t - q0) << 16) | (b0 - 3));
+                        i = t + b0;
+                        av = 0;
+                        continue;
                     }
+                    // whether t + 1 improves is not known here (cut or unevaluated): the general
+                    // step continues at t + 1 with t's match pending
+                    i = t + 1;
+                    ml = b0;
+                    ms = q0;
+                    av = 1;
+                    continue;
                 }
             }
+            count(9);
             const uint32_t pl = ml, pm = ms;
             ml = 2;
             if (i < npos && pl < 258) {
@@ -914,7 +986,9 @@ struct SmallWave {
                     const uint32_t e = group_get(g, i, npos, len);
                     uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
                     if (e >> 31) {
+                        stamp(2);
                         m = search(i, pl, len, m, q, &q);
+                        stamp(12);
                         count(15);
                     } else if (m <= pl) {
                         m = 0;
@@ -1020,7 +1094,7 @@ struct SmallWave {
         heap_len = rfl(heap_len + (d0 >= 0) + (d1 >= 0));
         max_code = rfl(max_code);
         wave_sync();
-        stamp(8);
+        stamp(3);
         // 2. heapify + merge (all uniform scalar control; the heap never leaves VGPRs)
         int node;
         bool deep = false;
@@ -1363,7 +1437,7 @@ struct SmallWave {
             opt_len = (int64_t)ol * 8 - 10;
             static_len = (int64_t)sl * 8 - 10;
         }
-        stamp(7);
+        stamp(3);
         PMC_STOP(7, bitpos)
         const uint32_t opt_lenb_raw = (uint32_t)(((uint64_t)opt_len + 3 + 7) >> 3);
         const uint32_t static_lenb = (uint32_t)(((uint64_t)static_len + 3 + 7) >> 3);
@@ -1578,15 +1652,19 @@ struct SmallWave {
         }
         wave_sync();
     }
+    // (PMC_STOP 11..14: front-kernel instruction attribution, see scripts/front_cost.sh)
     __device__ uint32_t run_front(const uint8_t *src, uint32_t len) {
         stage(src, len);
         stamp(0);
+        PMC_STOP(11, 0)
         const uint32_t npos = len >= 3 ? len - 2 : 0;
         uint32_t ntok;
         if (npos) {
             sort_positions2(npos, (PMC_LDS uint32_t *)CN);
             stamp(1);
+            PMC_STOP(12, 0)
             ntok = parse_ondemand(npos, len);
+            PMC_STOP(14, 0)
         } else {
             lit_run(0, 0, len);
             ntok = len;

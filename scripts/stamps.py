@@ -16,9 +16,9 @@ import pmc_codec  # noqa: E402
 from pmc_codec import device as D  # noqa: E402
 
 PHASES = ["stage+crc", "hash+sort", "parse", "trees lit+dist (rest)", "emit", "trailer+copy",
-          "zero+histogram", "runs+bl tree (rest)", "bt:leaves", "bt:heap", "bt:depths", "bt:sums", "bt:codes", "#groups",
+          "zero+histogram", "#tb_run iters", "#ext iters", "#general steps", "eval", "chain counts", "search", "#groups",
           "#parse steps", "#search calls"]
-COUNTS = {13, 14, 15}
+COUNTS = {7, 8, 9, 13, 14, 15}
 IPHASES = ["inf:stage+header", "inf:block hdr+code lens", "inf:table builds", "inf:symbol decode",
            "inf:materialise", "inf:crc+copy", "-", "-"]
 
