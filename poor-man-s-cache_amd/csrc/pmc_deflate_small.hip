@@ -105,6 +105,8 @@ uint64_t deflate_small_wave_bytes(uint64_t n) { return small_layout(n).total; }
 // histograms overlay S and R after the parse
 struct FrontLayout {
     uint64_t bytes, S, R, X, freq, total;
+    bool pk;             // chain counts packed into R's top 6 bits (n <= 1024: R < 1024)
+    uint64_t cn, hc, ev; // parse scratch in X (cn unused when pk); the sort's 512-B table at X
 };
 __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
     auto a = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
@@ -113,10 +115,14 @@ __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
     F.S = a(n + 32);
     F.R = F.S + a(2 * n + 2);
     F.X = F.R + a(2 * n + 2);
-    const uint64_t xs = cn_region_bytes(n) > 1024 ? cn_region_bytes(n) : 1024;
+    F.pk = n <= 1024;
+    F.cn = F.X;
+    F.hc = F.pk ? F.X : F.X + a(n);
+    F.ev = F.hc + a(((n + 63) / 64) * 8);
+    const uint64_t xe = F.ev + 320 > F.X + 512 ? F.ev + 320 : F.X + 512;
     F.freq = F.S;
-    const uint64_t t1 = F.X + xs, t2 = F.freq + 352 * 4;
-    F.total = a(t1 > t2 ? t1 : t2);
+    const uint64_t t2 = F.freq + 352 * 4;
+    F.total = a(xe > t2 ? xe : t2);
     return F;
 }
 uint64_t deflate_front_wave_bytes(uint64_t n) { return front_layout(n).total; }
@@ -268,6 +274,7 @@ struct SmallWave {
     PMC_LDS uint64_t *HC;   // on-demand parse: bit x = position x has a chain candidate (aliases M)
     PMC_LDS uint8_t *CN;    // on-demand parse: chain candidates of position x (capped at 255)
     PMC_LDS uint32_t *EV;   // on-demand parse: eval scratch (64 best keys, 64 u8 owner marks)
+    bool cnp;               // chain counts live in R's top 6 bits (values <= 1024 bytes), CN unused
     PMC_LDS uint64_t *ML;   // segment walk: positions that start a match (or are unresolved)
     PMC_LDS uint64_t *MP;   // segment walk: positions where a lazy-improvement run ends
     PMC_GLB uint32_t *tok;
@@ -370,29 +377,25 @@ struct SmallWave {
             const uint32_t sh = pass ? 8 : 0;
             const int nb = pass ? 7 : 8;
             PMC_LDS uint16_t *dst = pass ? S : Tt;
-            for (uint32_t k = l; k < 256; k += 64) tab[k] = 0;
+            // 256 u16 digit counters (512 B), counted two per word by u32 LDS atomics
+            PMC_LDS uint16_t *tab16 = (PMC_LDS uint16_t *)tab;
+            for (uint32_t k = l; k < 128; k += 64) tab[k] = 0;
             wave_sync();
             for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
                 const uint32_t x = c0 + l;
                 const bool valid = x < npos;
                 const uint32_t p = valid ? (pass ? (uint32_t)Tt[x] : x) : 0u;
                 const uint32_t d = (hash3(load4(p)) >> sh) & 255;
-                if (valid) lds_add(&tab[d], 1u);
+                if (valid) lds_add(&tab[d >> 1], 1u << (16 * (d & 1)));
             }
             wave_sync();
             {
-                uint32_t v[4], sum = 0;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    v[k] = tab[4 * l + k];
-                    sum += v[k];
-                }
-                uint32_t base = wave_incl_scan(sum) - sum;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    tab[4 * l + k] = base;
-                    base += v[k];
-                }
+                const uint32_t t0 = tab[2 * l], t1 = tab[2 * l + 1];
+                const uint32_t v0 = t0 & 0xffffu, v1 = t0 >> 16, v2 = t1 & 0xffffu, v3 = t1 >> 16;
+                const uint32_t sum = v0 + v1 + v2 + v3;
+                const uint32_t b0 = wave_incl_scan_dpp(sum) - sum, b1 = b0 + v0, b2 = b1 + v1, b3 = b2 + v2;
+                tab[2 * l] = b0 | b1 << 16;
+                tab[2 * l + 1] = b2 | b3 << 16;
             }
             wave_sync();
             for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
@@ -406,10 +409,10 @@ struct SmallWave {
                     m &= ((d >> bt) & 1) ? B : ~B;
                 }
                 const uint32_t rank = popc_lt(m);
-                const uint32_t at = tab[d];
+                const uint32_t at = tab16[d];
                 const bool last = valid && (l == 63 || (m >> (l + 1)) == 0);
                 if (valid) dst[at + rank] = (uint16_t)p;
-                if (last) tab[d] = at + rank + 1;
+                if (last) tab16[d] = (uint16_t)(at + rank + 1);
                 wave_sync();
             }
             wave_sync();
@@ -528,6 +531,7 @@ struct SmallWave {
     // Resumes a walk cut short by match_all: candidates kPreCand.. of position i, starting
     // from that walk's best / bestq.  Returns the match length (> b0) or 0; *q_out = the
     // nearest candidate achieving it.
+    template <bool PK>
     __device__ __forceinline__ uint32_t search(uint32_t i, uint32_t b0, uint32_t len, uint32_t best, uint32_t bestq,
                                uint32_t *q_out) {
         const int l = lane_id();
@@ -535,7 +539,7 @@ struct SmallWave {
         const uint32_t nice = (len - i) < 258 ? (len - i) : 258;
         const uint32_t wi = load4(i);
         const uint32_t hi = hash3(wi);
-        const int r = (int)R[i];
+        const int r = (int)(PK ? R[i] & 1023u : (uint32_t)R[i]);
         uint32_t examined = kPreCand;
         for (int kb = r - 1 - (int)kPreCand;; kb -= 64) {
             const uint32_t thr = best > b0 ? best : b0;
@@ -656,7 +660,7 @@ struct SmallWave {
                     const uint32_t e = rfl(M[i]);
                     uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
                     if (e >> 31) {
-                        m = search(i, prev_length, len, m, q, &q);
+                        m = search<false>(i, prev_length, len, m, q, &q);
                         count(15);
                     }
                     else if (m <= prev_length) m = 0;
@@ -705,6 +709,7 @@ struct SmallWave {
     // CN[x] = chain candidates of x = entries before x in its run of the hash-sorted order,
     // less position 0 (zlib's NIL: head[] value 0 never starts a match; the sort is stable,
     // so position 0 is the first entry of its run).  HC = CN > 0 as bits.
+    template <bool PK>
     __device__ __forceinline__ void build_cn(uint32_t npos) {
         const uint32_t l = (uint32_t)lane_id();
         const uint32_t k0 = rfl((uint32_t)R[0]);
@@ -719,14 +724,17 @@ struct SmallWave {
             uint32_t rs = wave_incl_max_dpp(valid && h != hp ? k : 0u);
             rs = rs > prs ? rs : prs;
             const uint32_t cnt = k - rs - (rs == k0 && k > rs ? 1u : 0u);
-            if (valid) CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
+            if (valid) {
+                if (PK) R[p] = (uint16_t)(k | (cnt < 63 ? cnt : 63) << 10);
+                else CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
+            }
             ph = readlane(h, 63);
             prs = readlane(rs, 63);
         }
         wave_sync();
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
             const uint32_t x = c0 + l;
-            const uint64_t m = ballot(x < npos && CN[x] != 0);
+            const uint64_t m = ballot(x < npos && (PK ? (R[x] >> 10) : (uint32_t)CN[x]) != 0);
             if (l == 0) HC[c0 >> 6] = m;
         }
         wave_sync();
@@ -756,12 +764,20 @@ struct SmallWave {
     // (4) 16 bytes at the candidate; then 16 bytes per step while some lane still matches;
     // (5) an LDS max per position and its read-back.  Lanes outside the evaluated prefix
     // compute on clamped indices and contribute key 0 (no exec-mask branches).
+    template <bool PK>
     __device__ void eval_group(Group &g, uint32_t p0, uint32_t npos, uint32_t len) {
         const uint32_t l = (uint32_t)lane_id();
         const uint32_t x = p0 + l;
-        const uint32_t xc = x < npos ? x : 0u;
-        uint32_t cn = CN[xc], cn1 = CN[x + 1 < npos ? x + 1 : 0u];
-        const uint32_t rx = R[xc];
+        const uint32_t xc = x < npos ? x : 0u, x1 = x + 1 < npos ? x + 1 : 0u;
+        uint32_t rx = R[xc], cn, cn1;
+        if (PK) {
+            cn = rx >> 10;
+            rx &= 1023u;
+            cn1 = (uint32_t)R[x1] >> 10;
+        } else {
+            cn = CN[xc];
+            cn1 = CN[x1];
+        }
         cn = x < npos ? cn : 0u;
         cn1 = x + 1 < npos ? cn1 : 0u;
         const uint32_t w = cn < kPreCand ? cn : kPreCand;
@@ -853,30 +869,33 @@ struct SmallWave {
         if (l < (t.n & 63)) tok[(t.n & ~63u) + l] = t.v;
     }
     // longest_match record of has-candidate position x (evaluating a new window if needed)
+    template <bool PK>
     __device__ uint32_t group_get(Group &g, uint32_t x, uint32_t npos, uint32_t len) {
         const uint32_t off = x - g.p0;
         if (off < 64 && ((g.m >> off) & 1)) return readlane(g.e, (int)off);
         stamp(2);
-        eval_group(g, x, npos, len);
+        eval_group<PK>(g, x, npos, len);
         stamp(10);
         count(13);
         return readlane(g.e, 0);
     }
     // (a noinline member reaches the wave state through `this`, a pointer to scratch: every
     // member pointer would be re-read from memory inside the loop.  A local copy lives in SGPRs.)
+    template <bool PK>
     __device__ __noinline__ uint32_t parse_ondemand(uint32_t npos_, uint32_t len_) {
         SmallWave me = *this;
-        const uint32_t r = me.parse_ondemand_body(npos_, len_);
+        const uint32_t r = me.parse_ondemand_body<PK>(npos_, len_);
 #ifdef PMC_STAMPS
         for (int k = 0; k < 16; k++) st[k] = me.st[k];
         t_last = me.t_last;
 #endif
         return r;
     }
+    template <bool PK>
     __device__ __forceinline__ uint32_t parse_ondemand_body(uint32_t npos_, uint32_t len_) {
         const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
         const uint32_t nw = (npos + 63) >> 6;
-        build_cn(npos);
+        build_cn<PK>(npos);
         stamp(11);
         PMC_STOP(13, 0)
         Group g;
@@ -929,7 +948,7 @@ struct SmallWave {
                 uint32_t off = i - g.p0;
                 if (!(off < 64 && ((g.m >> off) & 1))) {
                     stamp(2);
-                    eval_group(g, i, npos, len);
+                    eval_group<PK>(g, i, npos, len);
                     stamp(10);
                     count(13);
                     off = 0;
@@ -983,11 +1002,11 @@ struct SmallWave {
                     hcw = rfl64(HC[hci]);
                 }
                 if ((hcw >> (i & 63)) & 1) {
-                    const uint32_t e = group_get(g, i, npos, len);
+                    const uint32_t e = group_get<PK>(g, i, npos, len);
                     uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
                     if (e >> 31) {
                         stamp(2);
-                        m = search(i, pl, len, m, q, &q);
+                        m = search<PK>(i, pl, len, m, q, &q);
                         stamp(12);
                         count(15);
                     } else if (m <= pl) {
@@ -1663,7 +1682,7 @@ struct SmallWave {
             sort_positions2(npos, (PMC_LDS uint32_t *)CN);
             stamp(1);
             PMC_STOP(12, 0)
-            ntok = parse_ondemand(npos, len);
+            ntok = cnp ? parse_ondemand<true>(npos, len) : parse_ondemand<false>(npos, len);
             PMC_STOP(14, 0)
         } else {
             lit_run(0, 0, len);
@@ -1742,7 +1761,7 @@ struct SmallWave {
         // (len - 3); literal = its position (dist 0), the byte is fetched in flush.
         uint32_t ntok;
         if (npos) {
-            ntok = parse_ondemand(npos, len);
+            ntok = parse_ondemand<false>(npos, len);
         } else { // no position with MIN_MATCH lookahead: all literals
             lit_run(0, 0, len);
             ntok = len;
@@ -1809,6 +1828,7 @@ __device__ inline void small_wave_init(SmallWave &w, uint8_t *base, const SmallL
     w.cnt = to_lds<uint16_t>(base + L.cnt);
     w.M = to_lds<uint32_t>(base + L.M);
     w.CN = to_lds<uint8_t>(base + L.M);
+    w.cnp = false;
     w.HC = to_lds<uint64_t>(base + L.M + cn_hc_offset(a.cap_len));
     w.EV = to_lds<uint32_t>(base + L.M + cn_ev_offset(a.cap_len));
     w.crc_tab = to_lds<const uint32_t>((void *)crc_tab);
@@ -1858,6 +1878,7 @@ __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
     w.cnt = to_lds<uint16_t>(base + L.cnt);
     w.M = to_lds<uint32_t>(base + L.M);
     w.CN = to_lds<uint8_t>(base + L.M);
+    w.cnp = false;
     w.HC = to_lds<uint64_t>(base + L.M + cn_hc_offset(a.cap_len));
     w.EV = to_lds<uint32_t>(base + L.M + cn_ev_offset(a.cap_len));
     w.ML = to_lds<uint64_t>(base + L.masks);

@@ -28,7 +28,7 @@ namespace pmc {
 // interleaved by 64-value block (lane-coalesced).
 
 // ---- front -------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256, 6) deflate_front_kernel(DeflateArgs a) {
+__global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
     const uint64_t wave = (uint64_t)blockIdx.x * wpb + wib;
@@ -40,9 +40,10 @@ __global__ void __launch_bounds__(256, 6) deflate_front_kernel(DeflateArgs a) {
     small_wave_init(w, base, L, a, nullptr);
     w.S = to_lds<uint16_t>(base + F.S);
     w.R = to_lds<uint16_t>(base + F.R);
-    w.CN = to_lds<uint8_t>(base + F.X);
-    w.HC = to_lds<uint64_t>(base + F.X + cn_hc_offset(a.cap_len));
-    w.EV = to_lds<uint32_t>(base + F.X + cn_ev_offset(a.cap_len));
+    w.CN = to_lds<uint8_t>(base + F.cn);
+    w.HC = to_lds<uint64_t>(base + F.hc);
+    w.EV = to_lds<uint32_t>(base + F.ev);
+    w.cnp = F.pk;
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;
