@@ -33,10 +33,15 @@ constexpr int kLaneLitCap = 96, kLaneDistCap = 32;
 constexpr int kColLit = 0, kColDist = kColLit + kLaneLitCap, kColBaseL = kColDist + kLaneDistCap;
 constexpr int kColBaseD = kColBaseL + 16, kColWords = kColBaseD + 16;
 constexpr int kBColCntL = 0, kBColCntD = 16, kBColBaseC = 32, kBColCl = 40; // build columns
-constexpr uint32_t kLaneTabOff = (uint32_t)kColWords * 64 * 2;             // length/distance bases
-constexpr uint32_t kLaneRingOff = (kLaneTabOff + 64 * 4 + 255) & ~255u;    // output rings (LaneOut)
+#ifndef PMC_LANE_WIN
+#define PMC_LANE_WIN 16
+#endif
+// input window per lane (dwords, refilled by halves); 16 keeps a wave's LDS at 40 KiB, four
+// waves per CU (the kernel is latency-bound: its lanes wait on LDS and L2 most of the time)
+constexpr uint32_t kWinDw = PMC_LANE_WIN, kWinHalf = kWinDw / 2;
+constexpr uint32_t kLaneRingOff = (uint32_t)kColWords * 64 * 2;            // output rings (LaneOut)
 constexpr uint32_t kLaneWinOff = kLaneRingOff + 256 / 4 * 64 * 4;          // input windows (LaneWin)
-constexpr uint32_t kLaneLdsBytes = kLaneWinOff + 32 * 64 * 4;
+constexpr uint32_t kLaneLdsBytes = kLaneWinOff + kWinDw * 64 * 4;
 
 // 16-byte load through a global (not flat) pointer: flat loads also count against lgkmcnt,
 // so every LDS wait would wait for them too
@@ -102,8 +107,8 @@ struct LaneIn {
     }
 };
 
-// Bit reader of the decode loop: the next 32 dwords of the member sit in an LDS window
-// (column layout, stream dword j at slot j & 31).  Windows advance by 16 dwords for every
+// Bit reader of the decode loop: the next kWinDw dwords of the member sit in an LDS window
+// (column layout, stream dword j at slot j % kWinDw).  Windows advance by half for every
 // lane that can at the same time (wave-synchronous refill), so the wave waits on global
 // loads a few times per member instead of whenever any one lane's buffer runs low.
 struct LaneWin {
@@ -116,11 +121,11 @@ struct LaneWin {
     uint64_t buf;
     uint32_t n;
     __device__ uint4 block(uint32_t k) const { return k < nblk ? gload16(blk + k) : make_uint4(0, 0, 0, 0); }
-    __device__ void load16(uint32_t d0) { // dwords d0 .. d0 + 15 (d0 % 16 == 0) into their slots
+    __device__ void load_half(uint32_t d0) { // dwords d0 .. d0 + kWinHalf - 1 (aligned) into their slots
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
+        for (int b = 0; b < (int)kWinHalf / 4; b++) {
             const uint4 x = block(d0 / 4 + b);
-            const uint32_t s0 = (d0 + 4 * b) & 31;
+            const uint32_t s0 = (d0 + 4 * b) & (kWinDw - 1);
             w[(s0 + 0) * 64] = x.x;
             w[(s0 + 1) * 64] = x.y;
             w[(s0 + 2) * 64] = x.z;
@@ -133,9 +138,9 @@ struct LaneWin {
         nblk = (uint32_t)((((uintptr_t)in.p & 15) + in.len + 15) / 16);
         const uint64_t a = bp + head;
         nd = (uint32_t)(a >> 5);
-        wlo = nd & ~15u;
-        load16(wlo);
-        load16(wlo + 16);
+        wlo = nd & ~(kWinHalf - 1);
+        load_half(wlo);
+        load_half(wlo + kWinHalf);
         buf = 0;
         n = 0;
         refill();
@@ -143,16 +148,16 @@ struct LaneWin {
     }
     __device__ void refill() {
         if (n <= 32) {
-            buf |= (uint64_t)w[(nd & 31) * 64] << n;
+            buf |= (uint64_t)w[(nd & (kWinDw - 1)) * 64] << n;
             n += 32;
             nd++;
         }
     }
-    __device__ bool needs() const { return nd + 4 > wlo + 32; }
+    __device__ bool needs() const { return nd + 4 > wlo + kWinDw; }
     __device__ void advance() { // retire the older half of the window if it is consumed
-        if (nd >= wlo + 16) {
-            load16(wlo + 32);
-            wlo += 16;
+        if (nd >= wlo + kWinHalf) {
+            load_half(wlo + kWinDw);
+            wlo += kWinHalf;
         }
     }
     __device__ uint32_t peek(uint32_t k) const { return (uint32_t)buf & ((1u << k) - 1); }
