@@ -32,16 +32,23 @@ constexpr int kLaneLitCap = 96, kLaneDistCap = 32;
 // the output ring's bytes, which are only written once decoding starts.
 constexpr int kColLit = 0, kColDist = kColLit + kLaneLitCap, kColBaseL = kColDist + kLaneDistCap;
 constexpr int kColBaseD = kColBaseL + 16, kColWords = kColBaseD + 16;
-constexpr int kBColCntL = 0, kBColCntD = 16, kBColBaseC = 32, kBColCl = 40; // build columns
+constexpr int kBColCntL = 0, kBColCntD = 16, kBColBaseC = 32, kBColCl = 40; // build columns (+19)
 #ifndef PMC_LANE_WIN
 #define PMC_LANE_WIN 16
 #endif
-// input window per lane (dwords, refilled by halves); 16 keeps a wave's LDS at 40 KiB, four
-// waves per CU (the kernel is latency-bound: its lanes wait on LDS and L2 most of the time)
+// input window per lane (dwords, refilled by halves).  The kernel is latency-bound (its
+// lanes wait on LDS and L2 most of the time), so LDS per wave sets its speed through occupancy.
 constexpr uint32_t kWinDw = PMC_LANE_WIN, kWinHalf = kWinDw / 2;
+#ifndef PMC_LANE_RING
+#define PMC_LANE_RING 256
+#endif
+// output ring per lane (bytes; flushed by halves); matches reaching further back than
+// kRing - 16 read dst (L2).  (128 fits five waves per CU but measured slower than 256 at four.)
+constexpr uint32_t kRing = PMC_LANE_RING, kFlush = kRing / 2;
 constexpr uint32_t kLaneRingOff = (uint32_t)kColWords * 64 * 2;            // output rings (LaneOut)
-constexpr uint32_t kLaneWinOff = kLaneRingOff + 256 / 4 * 64 * 4;          // input windows (LaneWin)
+constexpr uint32_t kLaneWinOff = kLaneRingOff + kRing / 4 * 64 * 4;        // input windows (LaneWin)
 constexpr uint32_t kLaneLdsBytes = kLaneWinOff + kWinDw * 64 * 4;
+static_assert((kBColCl + 19) * 64 * 2 <= kRing * 64, "build columns live in the output rings");
 
 // 16-byte load through a global (not flat) pointer: flat loads also count against lgkmcnt,
 // so every LDS wait would wait for them too
@@ -354,7 +361,6 @@ __device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint16_t
 // dwords; complete dwords go to dst in bursts of >= kFlush bytes.  Keeping the byte-level
 // traffic in LDS keeps vmcnt free of thousands of byte stores (on gfx9 loads and stores
 // share it, so every later load would wait for them).
-constexpr uint32_t kRing = 256, kFlush = 128;
 struct LaneOut {
     PMC_LDS uint8_t *rb;  // byte view of the lane's ring column (byte q at (q >> 2) * 256 + (q & 3))
     PMC_LDS uint32_t *rw; // dword view (dword k at k * 64)
