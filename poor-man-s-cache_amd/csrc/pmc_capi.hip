@@ -151,6 +151,7 @@ struct pmc_ctx {
     DevBuf fbscratch;            // per-wave Trees for the small kernel's serial fallback
     DevBuf split;                // chunk arrays of the split small-value pipeline
     DevBuf crcx;                 // inflate: CRC-32 trailers from the lane kernel
+    DevBuf order;                // inflate: lane visit order (bins | member indices)
     bool prof = false;           // pmc_ctx_profile: bracket every launch with events
     struct KRec {
         int kind;
@@ -478,6 +479,19 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
         int r = ctx->crcx.ensure((uint64_t)n * 4);
         if (r) return r;
         a.crc_expect = (uint32_t *)ctx->crcx.p;
+        // visit order by compressed length (PMC_INFLATE_ORDER=0: index order)
+        static const bool no_order = getenv("PMC_INFLATE_ORDER") && !atoi(getenv("PMC_INFLATE_ORDER"));
+        if (!no_order && n >= 4096) {
+            r = ctx->order.ensure((uint64_t)kOrderBins * 4 + (uint64_t)n * 4);
+            if (r) return r;
+            uint32_t *bins = (uint32_t *)ctx->order.p, *ord = bins + kOrderBins;
+            HIP_TRY(hipMemsetAsync(bins, 0, kOrderBins * 4, st));
+            const unsigned ob = (unsigned)std::min<uint64_t>(((uint64_t)n + 1023) / 1024, (uint64_t)ctx->cus * 4);
+            hipLaunchKernelGGL(order_hist_kernel, dim3(ob), dim3(256), 0, st, src_len, (uint64_t)n, bins);
+            hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, st, bins);
+            hipLaunchKernelGGL(order_scatter_kernel, dim3(ob), dim3(256), 0, st, src_len, (uint64_t)n, bins, ord);
+            a.order = ord;
+        }
         const unsigned lb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * 16);
         klaunch(ctx, PMC_K_INFLATE_LANE, st,
                 [&] { hipLaunchKernelGGL(inflate_lane_kernel, dim3(lb), dim3(64), kLaneLdsBytes, st, a); });
@@ -485,6 +499,7 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
         klaunch(ctx, PMC_K_INFLATE_VERIFY, st,
                 [&] { hipLaunchKernelGGL(inflate_verify_kernel, dim3(vb), dim3(256), 0, st, a); });
         a.retry_only = 1;
+        a.order = nullptr;
     }
     // output image capacity for the LDS kernel; the compressed input of a member whose
     // output fits is at most gzip_bound(out) unless it is not a deflate member at all

@@ -415,7 +415,8 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
     PMC_LDS uint16_t *bcol = to_lds<uint16_t>((uint16_t *)((uint8_t *)lcol + kLaneRingOff) + threadIdx.x);
     PMC_LDS uint32_t *winw = to_lds<uint32_t>((uint8_t *)lcol + kLaneWinOff) + threadIdx.x;
     for (uint64_t vb = (uint64_t)blockIdx.x * 64; vb < a.n; vb += (uint64_t)gridDim.x * 64) {
-        const uint64_t v = vb + threadIdx.x;
+        const uint64_t vi = vb + threadIdx.x;
+        const uint64_t v = a.order && vi < a.n ? (uint64_t)a.order[vi] : vi;
         const uint32_t in_len = v < a.n ? a.src_len[v] : 0u;
         // st: 0 decoding, 1 end of block reached, 2 declined, 3 no member / empty input
         uint32_t st = v < a.n ? 0u : 3u;
@@ -434,7 +435,14 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
         dist.base = (PMC_LDS int16_t *)(col + kColBaseD * 64);
         dist.sym = col + kColDist * 64;
         bool fixed = false;
+#ifdef PMC_STAMPS
+        uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
         if (st == 0 && !lane_prepare(in, col, bcol, lit, dist, fixed)) st = 2;
+#ifdef PMC_STAMPS
+        uint64_t t1 = __builtin_amdgcn_s_memtime();
+        uint64_t n_it = 0, n_act = 0;
+#endif
         LaneWin win;
         win.w = winw;
         win.start(in, st == 0 ? in.bitpos() : 0);
@@ -450,6 +458,10 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
         uint32_t rem = 0, md = 0; // pending match: bytes left, distance
         // one step per iteration: a symbol, then up to 8 bytes of the current match
         while (ballot(st == 0)) {
+#ifdef PMC_STAMPS
+            n_it++;
+            n_act += __builtin_popcountll(ballot(st == 0));
+#endif
             if (ballot(st == 0 && win.needs()))
                 if (st == 0) win.advance();
             if (st == 0) {
@@ -508,6 +520,9 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
             if (ballot(st == 0 && o.pos - o.flushed >= kFlush))
                 if (st == 0) o.flush(o.pos, false);
         }
+#ifdef PMC_STAMPS
+        uint64_t t2 = __builtin_amdgcn_s_memtime();
+#endif
         if (st == 1) {
             if (win.bitpos() > (uint64_t)in.len * 8) st = 2;
         }
@@ -530,7 +545,64 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
             }
         }
         if (st == 2) a.rc[v] = kInflateRetry;
+#ifdef PMC_STAMPS
+        // dbg slots 3..7 (the wave kernels' 0..5 see only retried members): wave iterations
+        // of the decode loop, active lane-iterations, cycles in prepare, decode, finish
+        uint64_t t3 = __builtin_amdgcn_s_memtime();
+        if (threadIdx.x == 0 && a.dbg) {
+            atomicAdd((unsigned long long *)&a.dbg[3], (unsigned long long)n_it);
+            atomicAdd((unsigned long long *)&a.dbg[4], (unsigned long long)n_act);
+            atomicAdd((unsigned long long *)&a.dbg[5], (unsigned long long)(t1 - t0));
+            atomicAdd((unsigned long long *)&a.dbg[6], (unsigned long long)(t2 - t1));
+            atomicAdd((unsigned long long *)&a.dbg[7], (unsigned long long)(t3 - t2));
+        }
+#endif
     }
+}
+
+// ---- visit order: counting sort of member indices by compressed length ------------------
+// Blocks take contiguous slices; bins are per-block LDS counts, one global add per used bin.
+__device__ __forceinline__ uint32_t order_bin(uint32_t len) { return len < kOrderBins ? len : kOrderBins - 1; }
+__global__ void __launch_bounds__(256) order_hist_kernel(const uint32_t *src_len, uint64_t n, uint32_t *hist) {
+    __shared__ uint32_t h[kOrderBins];
+    for (uint32_t k = threadIdx.x; k < kOrderBins; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x, b0 = (uint64_t)blockIdx.x * per;
+    const uint64_t b1 = b0 + per < n ? b0 + per : n;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) atomicAdd(&h[order_bin(src_len[i])], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kOrderBins; k += blockDim.x)
+        if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+// exclusive scan of the bins in place (one block of 1024 threads, two bins each)
+__global__ void __launch_bounds__(1024) order_scan_kernel(uint32_t *hist) {
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x, a = hist[2 * t], b = hist[2 * t + 1];
+    part[t] = a + b;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint32_t v = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const uint32_t ex = part[t] - (a + b);
+    hist[2 * t] = ex;
+    hist[2 * t + 1] = ex + a;
+}
+__global__ void __launch_bounds__(256) order_scatter_kernel(const uint32_t *src_len, uint64_t n, uint32_t *cursor,
+                                                            uint32_t *order) {
+    __shared__ uint32_t h[kOrderBins];
+    for (uint32_t k = threadIdx.x; k < kOrderBins; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x, b0 = (uint64_t)blockIdx.x * per;
+    const uint64_t b1 = b0 + per < n ? b0 + per : n;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) atomicAdd(&h[order_bin(src_len[i])], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kOrderBins; k += blockDim.x)
+        if (h[k]) h[k] = atomicAdd(&cursor[k], h[k]); // this block's range in bin k
+    __syncthreads();
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) order[atomicAdd(&h[order_bin(src_len[i])], 1u)] = (uint32_t)i;
 }
 
 // CRC-32 of every member the lane kernel decoded (wave per member); a mismatch sends the

@@ -76,7 +76,15 @@ struct InflateArgs {
     uint64_t *dbg; // PMC_STAMPS builds: per-phase cycle sums (slots 0..7 deflate-independent)
     uint32_t *crc_expect; // lane kernel -> verify kernel: the member's CRC-32 trailer
     int32_t retry_only;   // wave kernels: only members the lane kernel marked kInflateRetry
+    const uint32_t *order; // lane kernel: member visit order (by compressed length), or null
 };
+
+// lane-inflate visit order: member indices grouped by compressed length, so a wave's 64
+// lanes decode members of similar length and finish their decode loops together
+constexpr uint32_t kOrderBins = 2048;
+__global__ void order_hist_kernel(const uint32_t *src_len, uint64_t n, uint32_t *hist);
+__global__ void order_scan_kernel(uint32_t *hist);
+__global__ void order_scatter_kernel(const uint32_t *src_len, uint64_t n, uint32_t *cursor, uint32_t *order);
 
 constexpr int32_t kInflateRetry = -7777; // internal rc: lane fast path declined the member
 

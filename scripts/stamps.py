@@ -19,8 +19,9 @@ PHASES = ["stage+crc", "hash+sort", "parse", "trees lit+dist (rest)", "emit", "t
           "zero+histogram", "#tb_run iters", "#ext iters", "#general steps", "eval", "chain counts", "search", "#groups",
           "#parse steps", "#search calls"]
 COUNTS = {7, 8, 9, 13, 14, 15}
-IPHASES = ["inf:stage+header", "inf:block hdr+code lens", "inf:table builds", "inf:symbol decode",
-           "inf:materialise", "inf:crc+copy", "-", "-"]
+IPHASES = ["inf:stage+header", "inf:block hdr+code lens", "inf:table builds", "lane:#decode iters (wave)",
+           "lane:#active lane-iters", "lane:prepare", "lane:decode loop", "lane:finish"]
+ICOUNTS = {3, 4}
 
 
 def main():
@@ -45,12 +46,13 @@ def main():
         torch.cuda.synchronize()
         s = dbg.cpu().tolist()
         for lo, names, what in ((0, PHASES, "deflate"), (16, IPHASES, "inflate")):
-            tot = sum(v for k, v in enumerate(s[lo:lo + 16]) if lo or k not in COUNTS)
+            cnt = COUNTS if lo == 0 else ICOUNTS
+            tot = sum(v for k, v in enumerate(s[lo:lo + 16]) if k not in cnt)
             bad = int((rc != 0).sum()) if lo == 0 else int((brc != 0).sum())
             print(f"vlen={vlen} kind={kind} n={n} {what}: wave-cycles/value total {tot / n:,.0f}  rc!=0: {bad}")
             for k, name in enumerate(names):
                 if s[lo + k]:
-                    pct = "" if (lo == 0 and k in COUNTS) else f"{100 * s[lo + k] / tot:5.1f}%"
+                    pct = "" if k in cnt else f"{100 * s[lo + k] / max(tot, 1):5.1f}%"
                     print(f"   {name:24s} {s[lo + k] / n:12,.1f}  {pct}")
     ctx.close()
 
