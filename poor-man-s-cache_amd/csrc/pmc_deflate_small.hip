@@ -256,6 +256,11 @@ struct TreeOut {
 };
 
 #define PMC_GLB __attribute__((address_space(1)))
+// chain candidates evaluated per position by the on-demand parse's wave step (the rest, when
+// needed, by search()); at most 32 (5-bit field in the eval key)
+#ifndef PMC_PRECAND
+#define PMC_PRECAND 32
+#endif
 struct SmallWave {
     // every working array is LDS-typed (ds_* with 32-bit addresses)
     PMC_LDS uint8_t *b;
@@ -462,7 +467,7 @@ struct SmallWave {
     // parallel before the serial parse.  M[i] = best | bestq << 9 | (walk cut short) << 31
     // with best = max over those candidates of min(LCP, nice), bestq the nearest achieving
     // it.  A cut-short walk is finished by search() if the parse visits i.
-    static constexpr uint32_t kPreCand = 32;
+    static constexpr uint32_t kPreCand = PMC_PRECAND;
     // Work-stealing walk, branch-light: every iteration each lane issues the same loads
     // (one chain entry, 8 bytes at i+off and at c+off, the two prune words) and advances
     // its state with selects -- a candidate is fetched, pruned, or compared 8 bytes further.

@@ -308,7 +308,7 @@ template __global__ void deflate_trees_kernel<kTreesCap>(DeflateArgs);
 template __global__ void deflate_trees_kernel<kLCodes>(DeflateArgs);
 
 // ---- back --------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256, 4) deflate_back_kernel(DeflateArgs a) {
+__global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
     for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
