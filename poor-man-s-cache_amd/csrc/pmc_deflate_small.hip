@@ -126,7 +126,26 @@ __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
     return F;
 }
 uint64_t deflate_front_wave_bytes(uint64_t n) { return front_layout(n).total; }
-uint64_t deflate_back_wave_bytes(uint64_t n) { return small_layout(n).back_total; }
+// split-pipeline back (emission only): bytes | out | lcode | dcode | blcode | runs | lengths
+struct BackLayout {
+    uint64_t bytes, out, out_words, lcode, dcode, blcode, runs, ls, blfreq, total;
+};
+__host__ __device__ inline BackLayout back_layout(uint64_t n) {
+    auto a = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
+    BackLayout B;
+    B.bytes = 0;
+    B.out = a(n + 32);
+    B.out_words = a(gzip_bound(n) + 16) / 4;
+    B.lcode = B.out + B.out_words * 4;
+    B.dcode = B.lcode + 288 * 4;
+    B.blcode = B.dcode + 32 * 4;
+    B.runs = B.blcode + 32 * 4;
+    B.ls = B.runs + 320 * 2;
+    B.blfreq = a(B.ls + kSplitRows); // scan_runs' bit-length counts (unused by the back)
+    B.total = B.blfreq + 32 * 4;
+    return B;
+}
+uint64_t deflate_back_wave_bytes(uint64_t n) { return back_layout(n).total; }
 
 __device__ __forceinline__ uint32_t hash3(uint32_t w) {
     return ((w & 0xff) << 10 ^ ((w >> 8) & 0xff) << 5 ^ ((w >> 16) & 0xff)) & 0x7fffu;

@@ -318,9 +318,20 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     uint8_t *base = lds + 1024 + (uint64_t)wib * a.wave_bytes;
     const SmallLayout L = small_layout(a.cap_len);
+    const BackLayout B = back_layout(a.cap_len);
     SmallWave w;
     small_wave_init(w, base, L, a, crc_tab);
-    PMC_LDS uint8_t *Ls = to_lds<uint8_t>(base + L.dad); // code lengths (dad/dep are unused here)
+    w.outw = to_lds<uint32_t>(base + B.out);
+    w.outb = to_lds<uint8_t>(base + B.out);
+    w.out_words = (uint32_t)B.out_words;
+    w.lcode = to_lds<uint32_t>(base + B.lcode);
+    w.dcode = to_lds<uint32_t>(base + B.dcode);
+    w.blcode = to_lds<uint32_t>(base + B.blcode);
+    w.runs = to_lds<uint16_t>(base + B.runs);
+    w.blfreq = to_lds<uint32_t>(base + B.blfreq);
+    // (run_back touches only the arrays above; the rest of w still points into the larger
+    // small_layout and must stay unused here)
+    PMC_LDS uint8_t *Ls = to_lds<uint8_t>(base + B.ls); // code lengths from the trees kernel
     for (uint64_t g = wave * 64; g < a.count; g += nwaves * 64) {
         const uint64_t vl = g + (uint64_t)l;
         const uint32_t myl = vl < a.count ? a.src_len[a.first + vl] : 0u;
