@@ -1267,13 +1267,36 @@ struct SmallWave {
             if (n18) lds_add(&blfreq[18], n18);
         }
     }
-    // bits of one run (send_tree); emit into the image at pos when out != nullptr
+    // bits of one run (send_tree), closed form of run_bits' count
+    __device__ uint32_t run_nbits(uint32_t v, uint32_t R) const {
+        const uint32_t Lv = blcode[v] >> 16;
+        if (v) {
+            const uint32_t L16 = (blcode[16] >> 16) + 2;
+            const uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = rem / 6, last = rem % 6;
+            uint32_t n = c1 < 4 ? c1 * Lv : Lv + L16;
+            n += full * L16;
+            n += last ? (last < 3 ? last * Lv : L16) : 0u;
+            return n;
+        }
+        const uint32_t L17 = (blcode[17] >> 16) + 3, L18 = (blcode[18] >> 16) + 7;
+        const uint32_t full = R / 138, last = R % 138;
+        return full * L18 + (last ? (last < 3 ? last * Lv : last <= 10 ? L17 : L18) : 0u);
+    }
+    // bits of one run (send_tree); emit into the image at pos when write (the run's codes are
+    // gathered in a 64-bit register and ORed into the image a register at a time)
     __device__ uint32_t run_bits(uint32_t v, uint32_t R, uint64_t pos, bool write) {
+        uint64_t accv = 0;
+        uint32_t accn = 0;
         auto put = [&](uint32_t c, uint32_t xv, uint32_t xn, uint32_t &acc) {
             uint32_t cw = blcode[c], cn = cw >> 16;
             if (write) {
-                uint64_t bits = (uint64_t)(cw & 0xffff) | ((uint64_t)xv << cn);
-                or_bits_lds(pos + acc, bits, (int)(cn + xn));
+                if (accn > 48) { // (one code with extra bits is at most 7 + 7 bits)
+                    or_bits_lds(pos + acc - accn, accv, (int)accn);
+                    accv = 0;
+                    accn = 0;
+                }
+                accv |= ((uint64_t)(cw & 0xffff) | ((uint64_t)xv << cn)) << accn;
+                accn += cn + xn;
             }
             acc += cn + xn;
         };
@@ -1307,6 +1330,7 @@ struct SmallWave {
                 }
             }
         }
+        if (write && accn) or_bits_lds(pos + acc - accn, accv, (int)accn);
         return acc;
     }
     __device__ void or_bits_lds(uint64_t pos, uint64_t v, int n) {
@@ -1324,6 +1348,7 @@ struct SmallWave {
     // scan_tree for lengths code[0..max_code]: records run lengths at run starts into
     // runR (u16) and adds the bl counts.  Chunks are walked back to front so each run
     // start knows where the next run begins.
+    template <bool COUNT = true>
     __device__ void scan_runs(PMC_LDS const uint32_t *code, int max_code, PMC_LDS uint16_t *runR) {
         const int l = lane_id();
         int next_start = max_code + 1;
@@ -1338,7 +1363,7 @@ struct SmallWave {
             const int nxt = above ? c0 + __builtin_ctzll(above) : next_start;
             if (start) {
                 runR[s] = (uint16_t)(nxt - s);
-                run_counts(v, (uint32_t)(nxt - s), blfreq);
+                if (COUNT) run_counts(v, (uint32_t)(nxt - s), blfreq);
             }
             if (m) next_start = c0 + __builtin_ctzll(m);
         }
@@ -1355,7 +1380,7 @@ struct SmallWave {
             const uint32_t vp = (in && s > 0) ? code[s - 1] >> 16 : 0xfffeu;
             const bool start = in && (s == 0 || v != vp);
             const uint32_t R = start ? runR[s] : 0u;
-            const uint32_t nb = start ? run_bits(v, R, 0, false) : 0u;
+            const uint32_t nb = start ? run_nbits(v, R) : 0u;
             const uint32_t incl = wave_incl_scan(nb);
             if (start) run_bits(v, R, base + incl - nb, true);
             base += readlane(incl, 63);
@@ -1602,6 +1627,52 @@ struct SmallWave {
         }
         wave_sync();
     }
+    // canonical codes (gen_codes) with same-length groups from 4 ballots per chunk: per length
+    // counts, then each symbol's rank in its group plus the length's running next code, both
+    // kept in tmp (32 words: counts, next codes)
+    __device__ __noinline__ void codes_from_lengths4(PMC_LDS const uint8_t *Ls, int elems, PMC_LDS uint32_t *code_out,
+                                                     PMC_LDS uint32_t *tmp) {
+        const uint32_t l = (uint32_t)lane_id();
+        if (l < 32) tmp[l] = 0;
+        wave_sync();
+        auto group = [&](uint32_t len, bool in) {
+            uint64_t m = ballot(in);
+#pragma unroll
+            for (int bt = 0; bt < 4; bt++) {
+                const uint64_t B = ballot((len >> bt) & 1);
+                m &= ((len >> bt) & 1) ? B : ~B;
+            }
+            return m;
+        };
+        for (int c0 = 0; c0 < elems; c0 += 64) {
+            const int s = c0 + (int)l;
+            const bool in = s < elems;
+            const uint32_t len = in ? Ls[s] : 0u;
+            const uint64_t m = group(len, in);
+            if (in && len && popc_lt(m) == 0) lds_add(&tmp[len], (uint32_t)__builtin_popcountll(m));
+        }
+        wave_sync();
+        if (l == 0) {
+            uint32_t code = 0;
+            for (int L = 1; L <= 15; L++) {
+                code = (code + (L > 1 ? tmp[L - 1] : 0u)) << 1;
+                tmp[16 + L] = code;
+            }
+        }
+        wave_sync();
+        for (int c0 = 0; c0 < elems; c0 += 64) {
+            const int s = c0 + (int)l;
+            const bool in = s < elems;
+            const uint32_t len = in ? Ls[s] : 0u;
+            const uint64_t m = group(len, in);
+            const uint32_t rank = popc_lt(m), mycode = len ? tmp[16 + len] + rank : 0u;
+            wave_sync();
+            const bool last = in && len && (m >> l) == 1; // highest lane of its group
+            if (last) tmp[16 + len] = mycode + 1;
+            if (in) code_out[s] = len ? ((__builtin_bitreverse32(mycode) >> (32 - len)) | (len << 16)) : 0u;
+            wave_sync();
+        }
+    }
     // the block as planned by deflate_trees_kernel: plan = type | l_max << 2 | d_max << 11 |
     // max_blindex << 16 (type 0 stored, 1 fixed, 2 dynamic); Ls = lit/len, dist, bl lengths
     __device__ uint64_t emit_planned(uint32_t ntok, uint32_t len, uint64_t bitpos, uint32_t plan,
@@ -1632,12 +1703,13 @@ struct SmallWave {
             wave_sync();
         } else {
             const int l_max = (int)((plan >> 2) & 511), d_max = (int)((plan >> 11) & 31), mbi = (int)((plan >> 16) & 31);
-            codes_from_lengths(Ls, kLCodes, lcode);
-            codes_from_lengths(Ls + kLCodes, kDCodes, dcode);
-            codes_from_lengths(Ls + kLCodes + kDCodes, kBLCodes, blcode);
+            codes_from_lengths4(Ls, kLCodes, lcode, blfreq); // (blfreq: free scratch in the back)
+            codes_from_lengths4(Ls + kLCodes, kDCodes, dcode, blfreq);
+            codes_from_lengths4(Ls + kLCodes + kDCodes, kBLCodes, blcode, blfreq);
+            PMC_STOP(23, bitpos)
             PMC_LDS uint16_t *runL = runs, *runD = runs + 288;
-            scan_runs(lcode, l_max, runL);
-            scan_runs(dcode, d_max, runD);
+            scan_runs<false>(lcode, l_max, runL); // (the bl tree came from the trees kernel)
+            scan_runs<false>(dcode, d_max, runD);
             wave_sync();
             const int lcodes = l_max + 1, dcodes = d_max + 1, blcodes = mbi + 1;
             if (l == 0) {
@@ -1652,6 +1724,7 @@ struct SmallWave {
             bitpos += send_runs(lcode, lcodes - 1, runL, bitpos);
             bitpos += send_runs(dcode, dcodes - 1, runD, bitpos);
             wave_sync();
+            PMC_STOP(24, bitpos)
         }
         bitpos = emit_symbols(ntok, bitpos);
         const uint32_t eob = lcode[kEndBlock];
@@ -1723,7 +1796,9 @@ struct SmallWave {
                             uint8_t *dst, uint32_t dst_cap, uint32_t *dst_len) {
         const int l = lane_id();
         stage(src, len);
+        PMC_STOP(21, 0)
         const uint32_t crc = wave_crc32(b, len, crc_tab);
+        PMC_STOP(22, 0)
         for (uint64_t k = l; k < out_words; k += 64) outw[k] = 0;
         wave_sync();
         if (l < 10) {
@@ -1733,6 +1808,9 @@ struct SmallWave {
         wave_sync();
         stamp(0);
         uint64_t bitpos = emit_planned(ntok, len, 80, plan, Ls);
+        PMC_STOP(23, 0)
+        PMC_STOP(24, 0)
+        PMC_STOP(25, 0)
         stamp(4);
         uint64_t nbytes = bitpos >> 3;
         if (l < 8) {

@@ -52,7 +52,10 @@ struct DeflateArgs {
 constexpr uint32_t kSplitRows = 336;  // 286 lit/len + 30 dist + 19 bit-length (+1)
 constexpr uint32_t kMergeRows = 572;  // 2 heap entries per merge, <= 285 merges
 constexpr uint32_t kPlanDeferred = 0xffffffffu;
-constexpr int kTreesCap = 96;         // lane heap capacity of the first trees pass
+#ifndef PMC_TREES_CAP
+#define PMC_TREES_CAP 96
+#endif
+constexpr int kTreesCap = PMC_TREES_CAP; // lane heap capacity of the first trees pass
 
 // bytes of chunk scratch per value of the split pipeline
 __host__ __device__ inline uint64_t split_value_bytes(uint64_t cap) {
