@@ -1381,7 +1381,7 @@ struct SmallWave {
             const bool start = in && (s == 0 || v != vp);
             const uint32_t R = start ? runR[s] : 0u;
             const uint32_t nb = start ? run_nbits(v, R) : 0u;
-            const uint32_t incl = wave_incl_scan(nb);
+            const uint32_t incl = wave_incl_scan_dpp(nb);
             if (start) run_bits(v, R, base + incl - nb, true);
             base += readlane(incl, 63);
         }
@@ -1419,7 +1419,7 @@ struct SmallWave {
                     nb += xd;
                 }
             }
-            const uint32_t incl = wave_incl_scan(nb);
+            const uint32_t incl = wave_incl_scan_dpp(nb);
             if (nb) or_bits_lds(bitpos + incl - nb, v, (int)nb);
             bitpos += readlane(incl, 63);
         }
@@ -1755,7 +1755,26 @@ struct SmallWave {
     __device__ void stage(const uint8_t *src, uint32_t len) {
         const int l = lane_id();
         const uint32_t padded = (len + 32) & ~3u;
-        if ((((uintptr_t)src) & 3) == 0) {
+        if ((((uintptr_t)src) & 15) == 0) {
+            // 16 bytes per lane per load (one HBM round trip per KiB), then the tail bytes
+            PMC_GLB const uint4 *s16 = (PMC_GLB const uint4 *)src;
+            const uint32_t full16 = len >> 4;
+            const uint32_t nw = padded / 4; // words to write (zero past the value)
+            for (uint32_t k = l; 4 * k < nw; k += 64) {
+                uint4 x = make_uint4(0, 0, 0, 0);
+                if (k < full16) {
+                    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                    const v4u y = *(PMC_GLB const v4u *)(s16 + k);
+                    x = make_uint4(y.x, y.y, y.z, y.w);
+                }
+                bw[4 * k] = x.x;
+                if (4 * k + 1 < nw) bw[4 * k + 1] = x.y;
+                if (4 * k + 2 < nw) bw[4 * k + 2] = x.z;
+                if (4 * k + 3 < nw) bw[4 * k + 3] = x.w;
+            }
+            wave_sync();
+            for (uint32_t k = full16 * 16 + l; k < len; k += 64) b[k] = src[k];
+        } else if ((((uintptr_t)src) & 3) == 0) {
             const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src);
             const uint32_t full = len >> 2;
             for (uint32_t k = l; k < padded / 4; k += 64) bw[k] = k < full ? s4[k] : 0u;
