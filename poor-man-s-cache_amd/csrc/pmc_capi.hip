@@ -359,7 +359,8 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
         chunk = (chunk + 63) & ~(uint64_t)63;
         const uint64_t blocks = chunk / 64;
         int r = ctx->split.ensure(chunk * cap * 4 + chunk * 4 + chunk * 4 + blocks * 64 * kSplitRows * 3 +
-                                  blocks * 64 * kMergeRows * 4 + (chunk + 1) * 4 + 1024);
+                                  blocks * 64 * kMergeRows * 4 + (chunk + 1) * 4 + chunk * 8 +
+                                  kOrderBins * 4 + 1024);
         if (r) return r;
         if (hbm_waves) {
             r = ctx->tokens.ensure(hbm_waves * kSlabSyms * sizeof(uint32_t));
@@ -381,6 +382,13 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
         a.cL = (uint8_t *)p;
         p += blocks * 64 * kSplitRows;
         a.cD = (uint32_t *)p;
+        p += (chunk + 1) * 4;
+        a.cZ = (uint32_t *)p;
+        p += chunk * 4;
+        uint32_t *ord = (uint32_t *)p;
+        p += chunk * 4;
+        uint32_t *obins = (uint32_t *)p;
+        static const bool no_order = getenv("PMC_TREES_ORDER") && !atoi(getenv("PMC_TREES_ORDER"));
         a.lds_max_len = lds_cut;
         a.cap_len = cap;
         const size_t tl_small = (size_t)(kTreesCap + 1) * 64 * 4 + 36 * 64 * 2;
@@ -396,6 +404,17 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
                                    dim3(64 * Lf.wpb), Lf.lds - kCrcTabBytes, st, a);
             });
             if (hipMemsetAsync(a.cD + a.count, 0, 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
+            // trees visit order by used literal/length symbols (PMC_TREES_ORDER=0: index order)
+            a.cO = nullptr;
+            if (!no_order && a.count >= 4096) {
+                if (hipMemsetAsync(obins, 0, kOrderBins * 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
+                const unsigned ob = (unsigned)std::min<uint64_t>((a.count + 1023) / 1024, (uint64_t)ctx->cus * 4);
+                hipLaunchKernelGGL(order_hist_kernel, dim3(ob), dim3(256), 0, st, (const uint32_t *)a.cZ, a.count, obins);
+                hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, st, obins);
+                hipLaunchKernelGGL(order_scatter_kernel, dim3(ob), dim3(256), 0, st, (const uint32_t *)a.cZ, a.count,
+                                   obins, ord);
+                a.cO = ord;
+            }
             klaunch(ctx, PMC_K_DEFLATE_TREES, st, [&] {
                 hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap>, dim3(tb), dim3(64), tl_small, st, a);
                 hipLaunchKernelGGL(deflate_trees_kernel<kLCodes>, dim3(std::min<unsigned>(tb, (unsigned)ctx->cus)),

@@ -59,9 +59,16 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
             const uint32_t ntok = w.run_front(a.src + a.src_off[gv], len);
             // histograms -> column v of the chunk's interleaved u16 table
-            for (int s = l; s < kLCodes + kDCodes; s += 64)
-                a.cH[v * kSplitRows + s] = (uint16_t)(s < kLCodes ? w.lfreq[s] : w.dfreq[s - kLCodes]);
-            if (l == 0) a.cN[v] = ntok;
+            uint32_t nz = 0;
+            for (int s = l; s < kLCodes + kDCodes; s += 64) {
+                const uint32_t f = s < kLCodes ? w.lfreq[s] : w.dfreq[s - kLCodes];
+                a.cH[v * kSplitRows + s] = (uint16_t)f;
+                nz += (uint32_t)__builtin_popcountll(ballot(s < kLCodes && f != 0));
+            }
+            if (l == 0) {
+                a.cN[v] = ntok;
+                a.cZ[v] = nz;
+            }
         }
     }
     small_wave_stamps_out(w, a);
@@ -250,7 +257,8 @@ struct LaneTrees {
 };
 
 template <int CAP>
-__device__ void trees_value(const DeflateArgs &a, uint64_t v, PMC_LDS uint32_t *col, PMC_LDS uint16_t *aux) {
+__device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC_LDS uint32_t *col,
+                            PMC_LDS uint16_t *aux) {
     const uint32_t len = a.src_len[a.first + v];
     if (len == 0 || len > a.lds_max_len) return;
     const Tables &TT = c_tables;
@@ -260,7 +268,7 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, PMC_LDS uint32_t *
     t.blf = aux + 16 * 64;
     t.hist = a.cH + v * kSplitRows;
     t.lens = a.cL + v * kSplitRows;
-    t.mg = a.cG + ((v >> 6) * kMergeRows) * 64 + (v & 63);
+    t.mg = a.cG + ((slot >> 6) * kMergeRows) * 64 + (slot & 63); // (by lane slot: coalesced)
     for (uint32_t s = 0; s < kSplitRows; s += 16) *reinterpret_cast<uint4 *>(t.lens + s) = make_uint4(0, 0, 0, 0);
     int64_t opt = 0, stat = 0;
     auto hist = [&](int s) -> uint32_t { return t.hist[s]; };
@@ -297,11 +305,13 @@ __global__ void __launch_bounds__(64) deflate_trees_kernel(DeflateArgs a) {
     PMC_LDS uint32_t *col = to_lds<uint32_t>(tl + l);
     PMC_LDS uint16_t *aux = to_lds<uint16_t>((uint16_t *)(tl + (CAP + 1) * 64) + l);
     if (CAP != kLCodes) {
-        const uint64_t v = (uint64_t)blockIdx.x * 64 + l;
-        if (v < a.count) trees_value<CAP>(a, v, col, aux);
+        // values in cO order: a wave's lanes get heaps of similar size and finish together
+        const uint64_t vi = (uint64_t)blockIdx.x * 64 + l;
+        if (vi < a.count) trees_value<CAP>(a, a.cO ? (uint64_t)a.cO[vi] : vi, vi, col, aux);
     } else {
         const uint32_t nd = a.cD[a.count];
-        for (uint32_t k = blockIdx.x * 64 + l; k < nd; k += gridDim.x * 64) trees_value<CAP>(a, a.cD[k], col, aux);
+        for (uint32_t k = blockIdx.x * 64 + l; k < nd; k += gridDim.x * 64)
+            trees_value<CAP>(a, a.cD[k], a.cD[k], col, aux);
     }
 }
 template __global__ void deflate_trees_kernel<kTreesCap>(DeflateArgs);

@@ -47,6 +47,8 @@ struct DeflateArgs {
     uint32_t *cP;  // block plan per value
     uint32_t *cG;  // trees kernel merge lists, interleaved [block][kMergeRows][64]
     uint32_t *cD;  // values deferred to the large-heap trees pass; their number at cD[count]
+    uint32_t *cZ;  // used literal/length symbols per value (front -> visit order of the trees)
+    uint32_t *cO;  // trees kernel visit order (values grouped by cZ), or null
 };
 
 constexpr uint32_t kSplitRows = 336;  // 286 lit/len + 30 dist + 19 bit-length (+1)
@@ -59,7 +61,7 @@ constexpr int kTreesCap = PMC_TREES_CAP; // lane heap capacity of the first tree
 
 // bytes of chunk scratch per value of the split pipeline
 __host__ __device__ inline uint64_t split_value_bytes(uint64_t cap) {
-    return cap * 4 + 4 + kSplitRows * 2 + kSplitRows + 4 + kMergeRows * 4 + 4;
+    return cap * 4 + 4 + kSplitRows * 2 + kSplitRows + 4 + kMergeRows * 4 + 4 + 8;
 }
 
 struct InflateArgs {
