@@ -135,6 +135,7 @@ int pmc_debug_stamps(pmc_ctx *ctx, uint64_t *dev_buf);
 #define PMC_K_INFLATE_HBM 6
 #define PMC_K_INFLATE_LANE 7   /* lane-per-member decode fast path                     */
 #define PMC_K_INFLATE_VERIFY 8 /* CRC-32 check of the fast path's output               */
+#define PMC_K_ORDER 9          /* lane visit-order counting sorts (trees, lane inflate)  */
 #define PMC_K_COUNT 10
 int pmc_ctx_profile(pmc_ctx *ctx, int enable);
 int pmc_ctx_kernel_times(pmc_ctx *ctx, double *ms, uint32_t *launches, int nkinds);

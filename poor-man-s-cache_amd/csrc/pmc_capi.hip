@@ -409,10 +409,13 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
             if (!no_order && a.count >= 4096) {
                 if (hipMemsetAsync(obins, 0, kOrderBins * 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
                 const unsigned ob = (unsigned)std::min<uint64_t>((a.count + 1023) / 1024, (uint64_t)ctx->cus * 4);
-                hipLaunchKernelGGL(order_hist_kernel, dim3(ob), dim3(256), 0, st, (const uint32_t *)a.cZ, a.count, obins);
-                hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, st, obins);
-                hipLaunchKernelGGL(order_scatter_kernel, dim3(ob), dim3(256), 0, st, (const uint32_t *)a.cZ, a.count,
-                                   obins, ord);
+                klaunch(ctx, PMC_K_ORDER, st, [&] {
+                    hipLaunchKernelGGL(order_hist_kernel, dim3(ob), dim3(256), 0, st, (const uint32_t *)a.cZ, a.count,
+                                       obins);
+                    hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, st, obins);
+                    hipLaunchKernelGGL(order_scatter_kernel, dim3(ob), dim3(256), 0, st, (const uint32_t *)a.cZ,
+                                       a.count, obins, ord);
+                });
                 a.cO = ord;
             }
             klaunch(ctx, PMC_K_DEFLATE_TREES, st, [&] {
@@ -506,9 +509,11 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
             uint32_t *bins = (uint32_t *)ctx->order.p, *ord = bins + kOrderBins;
             HIP_TRY(hipMemsetAsync(bins, 0, kOrderBins * 4, st));
             const unsigned ob = (unsigned)std::min<uint64_t>(((uint64_t)n + 1023) / 1024, (uint64_t)ctx->cus * 4);
-            hipLaunchKernelGGL(order_hist_kernel, dim3(ob), dim3(256), 0, st, src_len, (uint64_t)n, bins);
-            hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, st, bins);
-            hipLaunchKernelGGL(order_scatter_kernel, dim3(ob), dim3(256), 0, st, src_len, (uint64_t)n, bins, ord);
+            klaunch(ctx, PMC_K_ORDER, st, [&] {
+                hipLaunchKernelGGL(order_hist_kernel, dim3(ob), dim3(256), 0, st, src_len, (uint64_t)n, bins);
+                hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, st, bins);
+                hipLaunchKernelGGL(order_scatter_kernel, dim3(ob), dim3(256), 0, st, src_len, (uint64_t)n, bins, ord);
+            });
             a.order = ord;
         }
         const unsigned lb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * 16);
