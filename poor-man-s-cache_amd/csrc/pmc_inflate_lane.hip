@@ -204,6 +204,17 @@ struct LaneCode {
         }
         return left == 0;
     }
+    // symbol at the head of the bit buffer without consuming it; *len = its code length
+    template <class R>
+    __device__ uint32_t peek_sym(const R &in, uint32_t &len) const {
+        const uint32_t x = __builtin_bitreverse32(in.peek(15)) >> 17;
+        uint32_t L = 1;
+#pragma unroll
+        for (int j = 0; j < NL - 1; j++) L += x >= lim[j] ? 1u : 0u;
+        const int idx = (int)base[L * 64] + (int)(x >> (15 - L));
+        len = L;
+        return sym[idx * 64];
+    }
     template <class R>
     __device__ uint32_t decode(R &in) const {
         const uint32_t x = __builtin_bitreverse32(in.peek(15)) >> 17;
@@ -216,6 +227,25 @@ struct LaneCode {
     }
 };
 
+template <class R>
+__device__ __forceinline__ uint32_t fixed_peek(const R &in, uint32_t &len) {
+    const uint32_t x9 = __builtin_bitreverse32(in.peek(9)) >> 23;
+    uint32_t sym;
+    if ((x9 >> 2) < 24) {
+        sym = 256 + (x9 >> 2);
+        len = 7;
+    } else if ((x9 >> 1) < 192) {
+        sym = (x9 >> 1) - 48;
+        len = 8;
+    } else if ((x9 >> 1) < 200) {
+        sym = 280 + (x9 >> 1) - 192;
+        len = 8;
+    } else {
+        sym = 144 + x9 - 400;
+        len = 9;
+    }
+    return sym;
+}
 template <class R>
 __device__ __forceinline__ uint32_t fixed_lit(R &in) {
     const uint32_t x9 = __builtin_bitreverse32(in.peek(9)) >> 23;
@@ -469,8 +499,19 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
                     win.refill();
                     const uint32_t sy = fixed ? fixed_lit(win) : lit.decode(win);
                     if (sy < 256) {
-                        if (o.pos >= cap) st = 2;
-                        else o.put(o.pos++, sy);
+                        if (o.pos >= cap) {
+                            st = 2;
+                        } else {
+                            o.put(o.pos++, sy);
+                            // literals are most of the steps: take the next symbol too when it is
+                            // one (the refilled buffer still holds >= 17 bits, a full peek)
+                            uint32_t l2;
+                            const uint32_t s2 = fixed ? fixed_peek(win, l2) : lit.peek_sym(win, l2);
+                            if (s2 < 256 && o.pos < cap) {
+                                win.drop(l2);
+                                o.put(o.pos++, s2);
+                            }
+                        }
                     } else if (sy == 256) {
                         st = 1;
                     } else if (sy > 285) {
