@@ -510,6 +510,13 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
                             if (s2 < 256 && o.pos < cap) {
                                 win.drop(l2);
                                 o.put(o.pos++, s2);
+                                win.refill();
+                                uint32_t l3;
+                                const uint32_t s3 = fixed ? fixed_peek(win, l3) : lit.peek_sym(win, l3);
+                                if (s3 < 256 && o.pos < cap) {
+                                    win.drop(l3);
+                                    o.put(o.pos++, s3);
+                                }
                             }
                         }
                     } else if (sy == 256) {
