@@ -55,7 +55,7 @@ constexpr uint32_t kSplitRows = 336;  // 286 lit/len + 30 dist + 19 bit-length (
 constexpr uint32_t kMergeRows = 572;  // 2 heap entries per merge, <= 285 merges
 constexpr uint32_t kPlanDeferred = 0xffffffffu;
 #ifndef PMC_TREES_CAP
-#define PMC_TREES_CAP 96
+#define PMC_TREES_CAP 84
 #endif
 constexpr int kTreesCap = PMC_TREES_CAP; // lane heap capacity of the first trees pass
 
