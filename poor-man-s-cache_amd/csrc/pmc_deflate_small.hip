@@ -1403,19 +1403,19 @@ struct SmallWave {
                     v = c & 0xffff;
                     nb = c >> 16;
                 } else {
-                    const uint32_t code = TT.length_code[lc];
+                    const uint32_t code = len_code_cf(lc);
                     uint32_t c = lcode[code + kLiterals + 1];
                     v = c & 0xffff;
                     nb = c >> 16;
-                    const uint32_t xl = TT.extra_lbits[code];
-                    v |= (uint64_t)((lc - TT.base_length[code]) & ((1u << xl) - 1)) << nb;
+                    const uint32_t xl = len_extra_cf(code);
+                    v |= (uint64_t)((lc - len_base_cf(code)) & ((1u << xl) - 1)) << nb;
                     nb += xl;
-                    const uint32_t dm = dist - 1, dc = d_code(TT, dm);
+                    const uint32_t dm = dist - 1, dc = dist_code_cf(dm);
                     c = dcode[dc];
                     v |= (uint64_t)(c & 0xffff) << nb;
                     nb += c >> 16;
-                    const uint32_t xd = TT.extra_dbits[dc];
-                    v |= (uint64_t)((dm - TT.base_dist[dc]) & ((1u << xd) - 1)) << nb;
+                    const uint32_t xd = dist_extra_cf(dc);
+                    v |= (uint64_t)((dm - dist_base_cf(dc)) & ((1u << xd) - 1)) << nb;
                     nb += xd;
                 }
             }
@@ -1438,8 +1438,8 @@ struct SmallWave {
             if (dist == 0) {
                 lds_add(&lfreq[lc], 1u);
             } else {
-                lds_add(&lfreq[TT.length_code[lc] + kLiterals + 1], 1u);
-                lds_add(&dfreq[d_code(TT, dist - 1)], 1u);
+                lds_add(&lfreq[len_code_cf(lc) + kLiterals + 1], 1u);
+                lds_add(&dfreq[dist_code_cf(dist - 1)], 1u);
             }
         }
         if (l == 0) lfreq[kEndBlock] = 1;
@@ -1585,8 +1585,8 @@ struct SmallWave {
             if (dist == 0) {
                 lds_add(&lfreq[lc], 1u);
             } else {
-                lds_add(&lfreq[TT.length_code[lc] + kLiterals + 1], 1u);
-                lds_add(&dfreq[d_code(TT, dist - 1)], 1u);
+                lds_add(&lfreq[len_code_cf(lc) + kLiterals + 1], 1u);
+                lds_add(&dfreq[dist_code_cf(dist - 1)], 1u);
             }
         }
         if (l == 0) lfreq[kEndBlock] = 1;

@@ -109,6 +109,30 @@ PMC_HD inline unsigned d_code(const Tables &T, unsigned dist) {
     return dist < 256 ? T.dist_code[dist] : T.dist_code[256 + (dist >> 7)];
 }
 
+// Closed forms of trees.c's _length_code / base_length / extra_lbits and _dist_code / base_dist /
+// extra_dbits (RFC 1951 3.2.5; equal to the tables entry for entry, checked by the parity tests).
+// They replace per-lane indexed loads from constant memory with a few VALU operations.
+PMC_HD inline unsigned log2_floor(unsigned x) { return 31u - (unsigned)__builtin_clz(x | 1u); }
+// length code (0..28) of lc = match length - 3 (0..255)
+PMC_HD inline unsigned len_code_cf(unsigned lc) {
+    if (lc < 8) return lc;
+    if (lc == 255) return 28;
+    const unsigned lx = log2_floor(lc) - 2;
+    return 4 * lx + (lc >> lx);
+}
+PMC_HD inline unsigned len_extra_cf(unsigned c) { return c < 8 || c == 28 ? 0u : (c - 4) >> 2; }
+PMC_HD inline unsigned len_base_cf(unsigned c) {
+    return c < 8 ? c : c == 28 ? 255u : (4 + (c & 3)) << ((c - 4) >> 2);
+}
+// distance code (0..29) of dm = distance - 1 (0..32767)
+PMC_HD inline unsigned dist_code_cf(unsigned dm) {
+    if (dm < 4) return dm;
+    const unsigned k = log2_floor(dm);
+    return 2 * k + ((dm >> (k - 1)) & 1);
+}
+PMC_HD inline unsigned dist_extra_cf(unsigned dc) { return dc < 4 ? 0u : (dc >> 1) - 1; }
+PMC_HD inline unsigned dist_base_cf(unsigned dc) { return dc < 4 ? dc : (2 + (dc & 1)) << ((dc >> 1) - 1); }
+
 // Per-wave Huffman workspace (4448 bytes).  Lives in LDS on the GPU.
 struct Trees {
     CtData ltree[kHeapSize];       // dyn_ltree

@@ -33,3 +33,14 @@ def test_host_pipeline_matches_goldens(golden, host_bin, mode):
             if f.read() != g:
                 bad.append(k)
     assert not bad, bad[:10]
+
+
+def test_closed_form_code_tables():
+    """The closed forms the kernels use for trees.c's length/distance code tables equal the
+    tables zlib builds (tests/host/closed_forms_check.cpp, every entry)."""
+    d = tempfile.mkdtemp(prefix="pmc_cf_")
+    exe = os.path.join(d, "closed_forms_check")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-o", exe,
+                           os.path.join(HERE, "host", "closed_forms_check.cpp")])
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
