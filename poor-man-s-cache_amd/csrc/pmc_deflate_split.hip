@@ -114,9 +114,19 @@ struct LaneTrees {
     // build_tree + gen_bitlen (trees.c) for one tree whose frequencies are freq(s), s < elems;
     // leaf lengths go to lens[row0 + s].  Returns max_code (-1 and `deferred` when the
     // heap would exceed CAP entries).
+    // kind: 0 lit/len, 1 distance, 2 bit-length tree.  Extra bits and the static trees' code
+    // lengths are closed forms (a per-lane indexed load from constant memory per leaf was a
+    // vector-memory round trip inside this serial loop).
+    __device__ static uint32_t xbits(int kind, uint32_t x) {
+        return kind == 0 ? (x >= kLiterals + 1 ? len_extra_cf(x - (kLiterals + 1)) : 0u)
+               : kind == 1 ? dist_extra_cf(x)
+                           : (x == 16 ? 2u : x == 17 ? 3u : x == 18 ? 7u : 0u);
+    }
+    __device__ static uint32_t static_len(int kind, uint32_t x) { // static_ltree / static_dtree .Len
+        return kind == 1 ? 5u : x < 144 ? 8u : x < 256 ? 9u : x < 280 ? 7u : 8u;
+    }
     template <class Freq>
-    __device__ int build(Freq freq, int elems, uint32_t row0, const CtData *stree, const uint8_t *extra, int extra_base,
-                         int max_length, int64_t &opt, int64_t &stat) {
+    __device__ int build(Freq freq, int elems, uint32_t row0, int kind, int max_length, int64_t &opt, int64_t &stat) {
         int heap_len = 0, max_code = -1;
         // (frequencies fetched 8 at a time so the loads overlap)
         for (int n0 = 0; n0 < elems; n0 += 8) {
@@ -139,7 +149,7 @@ struct LaneTrees {
             const int node = max_code < 2 ? ++max_code : 0;
             setH(++heap_len, 1u << 15 | (uint32_t)node);
             opt--;
-            if (stree) stat -= stree[node].dl;
+            if (kind != 2) stat -= static_len(kind, (uint32_t)node);
         }
         for (int n = heap_len / 2; n >= 1; n--) down((uint32_t)n, (uint32_t)heap_len);
         uint32_t node = (uint32_t)elems, nm = 0;
@@ -180,9 +190,9 @@ struct LaneTrees {
                     lens[row0 + x] = (uint8_t)bits;
                     blc[bits * 64]++;
                     const uint32_t f = key >> 15;
-                    const uint32_t xb = (int)x >= extra_base ? extra[x - extra_base] : 0u;
+                    const uint32_t xb = xbits(kind, x);
                     opt += (int64_t)f * (bits + xb);
-                    if (stree) stat += (int64_t)f * (stree[x].dl + xb);
+                    if (kind != 2) stat += (int64_t)f * (static_len(kind, x) + xb);
                 }
             }
         }
@@ -256,12 +266,15 @@ struct LaneTrees {
     }
 };
 
+// trees.c bl_order[i] from two packed constants (5-bit fields): no constant-memory load
+__device__ __forceinline__ uint32_t bl_order_cf(int i) {
+    return i < 12 ? (uint32_t)(0x22caa324e804a30ull >> (5 * i)) & 31u : (uint32_t)(0x3c2e1346cull >> (5 * (i - 12))) & 31u;
+}
 template <int CAP>
 __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC_LDS uint32_t *col,
                             PMC_LDS uint16_t *aux) {
     const uint32_t len = a.src_len[a.first + v];
     if (len == 0 || len > a.lds_max_len) return;
-    const Tables &TT = c_tables;
     LaneTrees<CAP> t;
     t.hp = col;
     t.blc = aux;
@@ -272,22 +285,22 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC
     for (uint32_t s = 0; s < kSplitRows; s += 16) *reinterpret_cast<uint4 *>(t.lens + s) = make_uint4(0, 0, 0, 0);
     int64_t opt = 0, stat = 0;
     auto hist = [&](int s) -> uint32_t { return t.hist[s]; };
-    const int l_max = t.build(hist, kLCodes, 0, TT.static_ltree, TT.extra_lbits, kLiterals + 1, kMaxBits, opt, stat);
+    const int l_max = t.build(hist, kLCodes, 0, 0, kMaxBits, opt, stat);
     if (t.deferred) {
         a.cP[v] = kPlanDeferred;
         a.cD[atomicAdd(a.cD + a.count, 1u)] = (uint32_t)v;
         return;
     }
     auto dhist = [&](int s) -> uint32_t { return t.hist[kLCodes + s]; };
-    const int d_max = t.build(dhist, kDCodes, kLCodes, TT.static_dtree, TT.extra_dbits, 0, kMaxBits, opt, stat);
+    const int d_max = t.build(dhist, kDCodes, kLCodes, 1, kMaxBits, opt, stat);
     for (int s = 0; s < kBLCodes; s++) t.blf[s * 64] = 0;
     t.scan(0, l_max);
     t.scan(kLCodes, d_max);
     auto bfreq = [&](int s) -> uint32_t { return t.blf[s * 64]; };
-    t.build(bfreq, kBLCodes, kLCodes + kDCodes, nullptr, TT.extra_blbits, 0, kMaxBLBits, opt, stat);
+    t.build(bfreq, kBLCodes, kLCodes + kDCodes, 2, kMaxBLBits, opt, stat);
     int mbi;
     for (mbi = kBLCodes - 1; mbi >= 3; mbi--)
-        if (t.lens[kLCodes + kDCodes + TT.bl_order[mbi]] != 0) break;
+        if (t.lens[kLCodes + kDCodes + bl_order_cf(mbi)] != 0) break;
     opt += 3 * ((int64_t)mbi + 1) + 5 + 5 + 4;
     uint32_t opt_lenb = (uint32_t)(((uint64_t)opt + 3 + 7) >> 3);
     const uint32_t static_lenb = (uint32_t)(((uint64_t)stat + 3 + 7) >> 3);
