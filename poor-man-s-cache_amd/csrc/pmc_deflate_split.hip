@@ -266,10 +266,6 @@ struct LaneTrees {
     }
 };
 
-// trees.c bl_order[i] from two packed constants (5-bit fields): no constant-memory load
-__device__ __forceinline__ uint32_t bl_order_cf(int i) {
-    return i < 12 ? (uint32_t)(0x22caa324e804a30ull >> (5 * i)) & 31u : (uint32_t)(0x3c2e1346cull >> (5 * (i - 12))) & 31u;
-}
 template <int CAP>
 __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC_LDS uint32_t *col,
                             PMC_LDS uint16_t *aux) {

@@ -328,7 +328,7 @@ __device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint16_t
     if (nlit > 286 || ndist > 30) return false;
     // code-length code: lengths (3 bits each, permuted order), counts, list
     uint64_t cll = 0;
-    for (uint32_t k = 0; k < ncl; k++) cll |= (uint64_t)in.bits(3) << (3 * c_cl_order[k]);
+    for (uint32_t k = 0; k < ncl; k++) cll |= (uint64_t)in.bits(3) << (3 * bl_order_cf((int)k));
     for (int L = 0; L < 16; L++) bcol[(kBColCntL + L) * 64] = 0;
     for (uint32_t sy = 0; sy < 19; sy++) {
         const uint32_t L = (uint32_t)(cll >> (3 * sy)) & 7;

@@ -132,6 +132,10 @@ PMC_HD inline unsigned dist_code_cf(unsigned dm) {
 }
 PMC_HD inline unsigned dist_extra_cf(unsigned dc) { return dc < 4 ? 0u : (dc >> 1) - 1; }
 PMC_HD inline unsigned dist_base_cf(unsigned dc) { return dc < 4 ? dc : (2 + (dc & 1)) << ((dc >> 1) - 1); }
+// trees.c bl_order[i] (= inflate's code-length order) from two packed constants of 5-bit fields
+PMC_HD inline unsigned bl_order_cf(int i) {
+    return i < 12 ? (unsigned)(0x22caa324e804a30ull >> (5 * i)) & 31u : (unsigned)(0x3c2e1346cull >> (5 * (i - 12))) & 31u;
+}
 
 // Per-wave Huffman workspace (4448 bytes).  Lives in LDS on the GPU.
 struct Trees {

@@ -1,6 +1,6 @@
 // CPU check: the closed forms of trees.c's length / distance code tables in pmc_trees.hpp
-// (len_code_cf, len_base_cf, len_extra_cf, dist_code_cf, dist_base_cf, dist_extra_cf) equal
-// the tables zlib 1.2.11 builds in tr_static_init (trees.c), entry for entry.
+// (len_code_cf, len_base_cf, len_extra_cf, dist_code_cf, dist_base_cf, dist_extra_cf, bl_order_cf)
+// equal the tables zlib 1.2.11 builds in tr_static_init (trees.c) and its bl_order, entry for entry.
 #include <cstdio>
 
 #include "../../poor-man-s-cache_amd/csrc/pmc_trees.hpp"
@@ -36,6 +36,8 @@ int main() {
         bad += dist_code_cf(dm) != (dm < 256 ? dist_code[dm] : dist_code[256 + (dm >> 7)]);
     for (unsigned dc = 0; dc < 30; dc++)
         bad += dist_base_cf(dc) != (unsigned)base_dist[dc] || dist_extra_cf(dc) != (unsigned)extra_dbits[dc];
+    static const int bl_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    for (int i = 0; i < 19; i++) bad += bl_order_cf(i) != (unsigned)bl_order[i];
     printf("closed forms: %d mismatches\n", bad);
     return bad != 0;
 }
