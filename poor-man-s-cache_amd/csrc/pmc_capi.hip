@@ -360,7 +360,7 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
         const uint64_t blocks = chunk / 64;
         int r = ctx->split.ensure(chunk * cap * 4 + chunk * 4 + chunk * 4 + blocks * 64 * kSplitRows * 3 +
                                   blocks * 64 * kMergeRows * 4 + (chunk + 1) * 4 + chunk * 8 +
-                                  kOrderBins * 4 + 1024);
+                                  kOrderBins * 4 + 64 + 1024);
         if (r) return r;
         if (hbm_waves) {
             r = ctx->tokens.ensure(hbm_waves * kSlabSyms * sizeof(uint32_t));
@@ -388,6 +388,8 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
         uint32_t *ord = (uint32_t *)p;
         p += chunk * 4;
         uint32_t *obins = (uint32_t *)p;
+        p += kOrderBins * 4;
+        a.cQ = (uint32_t *)p;
         static const bool no_order = getenv("PMC_TREES_ORDER") && !atoi(getenv("PMC_TREES_ORDER"));
         a.lds_max_len = lds_cut;
         a.cap_len = cap;
@@ -398,6 +400,7 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
             a.count = std::min<uint64_t>(chunk, n - first);
             const unsigned tb = (unsigned)((a.count + 63) / 64);
             a.wave_bytes = fwb;
+            if (hipMemsetAsync(a.cQ, 0, 8, st) != hipSuccess) return PMC_E_NO_DEVICE;
             klaunch(ctx, PMC_K_DEFLATE_FRONT, st, [&] {
                 hipLaunchKernelGGL(deflate_front_kernel,
                                    dim3((unsigned)std::min<uint64_t>(Lf.blocks, (a.count + Lf.wpb - 1) / Lf.wpb)),

@@ -31,8 +31,6 @@ namespace pmc {
 __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
-    const uint64_t wave = (uint64_t)blockIdx.x * wpb + wib;
-    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     uint8_t *base = lds + (uint64_t)wib * a.wave_bytes;
     const SmallLayout L = small_layout(a.cap_len);
     const FrontLayout F = front_layout(a.cap_len);
@@ -47,15 +45,18 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;
-    for (uint64_t g = wave * 64; g < a.count; g += nwaves * 64) {
-        const uint64_t vl = g + (uint64_t)l;
-        const uint32_t myl = vl < a.count ? a.src_len[a.first + vl] : 0u;
-        uint64_t todo = ballot(vl < a.count && myl != 0 && myl <= a.lds_max_len);
-        while (todo) {
-            const int j = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const uint64_t v = g + (uint64_t)j, gv = a.first + v;
-            const uint32_t len = readlane(myl, j);
+    // Values come from a work counter, one at a time, the next one fetched while this one
+    // runs: value costs vary, and a static split left waves idle (a chunk of 555K values over
+    // 7168 resident waves is 1.2 rounds of 64-value groups).
+    uint32_t nx = l == 0 ? atomicAdd(a.cQ, 1u) : 0u;
+    for (;;) {
+        const uint64_t v = readlane(nx, 0);
+        if (v >= a.count) break;
+        nx = l == 0 ? atomicAdd(a.cQ, 1u) : 0u;
+        const uint64_t gv = a.first + v;
+        const uint32_t len = rfl(a.src_len[gv]);
+        if (len == 0 || len > a.lds_max_len) continue;
+        {
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
             const uint32_t ntok = w.run_front(a.src + a.src_off[gv], len);
             // histograms -> column v of the chunk's interleaved u16 table
@@ -333,8 +334,6 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
     for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
     __syncthreads();
     const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
-    const uint64_t wave = (uint64_t)blockIdx.x * wpb + wib;
-    const uint64_t nwaves = (uint64_t)gridDim.x * wpb;
     uint8_t *base = lds + 1024 + (uint64_t)wib * a.wave_bytes;
     const SmallLayout L = small_layout(a.cap_len);
     const BackLayout B = back_layout(a.cap_len);
@@ -351,10 +350,19 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
     // (run_back touches only the arrays above; the rest of w still points into the larger
     // small_layout and must stay unused here)
     PMC_LDS uint8_t *Ls = to_lds<uint8_t>(base + B.ls); // code lengths from the trees kernel
-    for (uint64_t g = wave * 64; g < a.count; g += nwaves * 64) {
+    // (work counter as in the front, in batches of 16 values whose lengths, token counts and
+    // plans load together: a back value is short, and a round trip per value showed)
+    constexpr uint32_t kBatch = 16;
+    uint32_t nx = l == 0 ? atomicAdd(a.cQ + 1, kBatch) : 0u;
+    for (;;) {
+        const uint64_t g = readlane(nx, 0);
+        if (g >= a.count) break;
+        nx = l == 0 ? atomicAdd(a.cQ + 1, kBatch) : 0u;
         const uint64_t vl = g + (uint64_t)l;
-        const uint32_t myl = vl < a.count ? a.src_len[a.first + vl] : 0u;
-        uint64_t todo = ballot(vl < a.count && myl <= a.lds_max_len);
+        const bool in = (uint32_t)l < kBatch && vl < a.count;
+        const uint32_t myl = in ? a.src_len[a.first + vl] : 0u;
+        const uint32_t myn = in ? a.cN[vl] : 0u, myp = in ? a.cP[vl] : 0u;
+        uint64_t todo = ballot(in && myl <= a.lds_max_len);
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -367,7 +375,7 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
                 }
                 continue;
             }
-            const uint32_t ntok = a.cN[v], plan = a.cP[v];
+            const uint32_t ntok = readlane(myn, j), plan = readlane(myp, j);
             for (uint32_t s = l; s < kSplitRows; s += 64) Ls[s] = a.cL[v * kSplitRows + s];
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
             const int rc = w.run_back(a.src + a.src_off[gv], len, ntok, plan, Ls, a.dst + a.dst_off[gv],

@@ -49,6 +49,7 @@ struct DeflateArgs {
     uint32_t *cD;  // values deferred to the large-heap trees pass; their number at cD[count]
     uint32_t *cZ;  // used literal/length symbols per value (front -> visit order of the trees)
     uint32_t *cO;  // trees kernel visit order (values grouped by cZ), or null
+    uint32_t *cQ;  // work counters of the front [0] and back [1] kernels (zeroed per chunk)
 };
 
 constexpr uint32_t kSplitRows = 336;  // 286 lit/len + 30 dist + 19 bit-length (+1)
