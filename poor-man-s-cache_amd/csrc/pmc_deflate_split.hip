@@ -48,15 +48,23 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     // Values come from a work counter, one at a time, the next one fetched while this one
     // runs: value costs vary, and a static split left waves idle (a chunk of 555K values over
     // 7168 resident waves is 1.2 rounds of 64-value groups).
-    uint32_t nx = l == 0 ? atomicAdd(a.cQ, 1u) : 0u;
+#ifndef PMC_FRONT_BATCH
+#define PMC_FRONT_BATCH 1
+#endif
+    constexpr uint32_t kBatch = PMC_FRONT_BATCH;
+    uint32_t nx = l == 0 ? atomicAdd(a.cQ, kBatch) : 0u;
     for (;;) {
-        const uint64_t v = readlane(nx, 0);
-        if (v >= a.count) break;
-        nx = l == 0 ? atomicAdd(a.cQ, 1u) : 0u;
-        const uint64_t gv = a.first + v;
-        const uint32_t len = rfl(a.src_len[gv]);
-        if (len == 0 || len > a.lds_max_len) continue;
-        {
+        const uint64_t g = readlane(nx, 0);
+        if (g >= a.count) break;
+        nx = l == 0 ? atomicAdd(a.cQ, kBatch) : 0u;
+        const uint64_t vl = g + (uint64_t)l;
+        const uint32_t myl = (uint32_t)l < kBatch && vl < a.count ? a.src_len[a.first + vl] : 0u;
+        uint64_t todo = ballot(myl != 0 && myl <= a.lds_max_len);
+        while (todo) {
+            const int jj = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint64_t v = g + (uint64_t)jj, gv = a.first + v;
+            const uint32_t len = readlane(myl, jj);
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
             const uint32_t ntok = w.run_front(a.src + a.src_off[gv], len);
             // histograms -> column v of the chunk's interleaved u16 table
