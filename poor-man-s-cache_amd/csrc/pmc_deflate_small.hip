@@ -847,22 +847,31 @@ struct SmallWave {
         wave_sync();
         const uint32_t kk = EV[l], best = kk >> 23;
         const uint32_t nx = (len - x) < 258 ? (len - x) : 258;
-        const bool cut = cn > kPreCand && best < nx;
-        const uint32_t bq = kk & 0x3fffu, e = best | bq << 9 | (cut ? 1u << 31 : 0u);
+        auto neg = [](uint32_t d) { return d >> 31; }; // 1 iff d < 0 as int (all values here are small)
+        uint32_t cutc = neg(kPreCand - cn) & neg(best - nx);
+        const uint32_t bq = kk & 0x3fffu, e = best | bq << 9 | cutc << 31;
         g.p0 = p0;
         g.m = im;
         g.e = e;
-        // walk masks (the fast path of deflate_slow, per offset); e of offset l + 1 via DPP
-        const bool ev = (im >> l) & 1;
-        const bool usable = best >= 4 || (best == 3 && x - bq <= 4096); // TOO_FAR
+        // Walk masks (the fast path of deflate_slow, per offset); e of offset l + 1 via DPP.
+        // The conditions are 0/1 integers (sign bits of differences of small values), so they
+        // combine on the vector ALU: as bools they became lane-mask logic on the scalar unit,
+        // which this kernel saturates.
         const uint32_t en = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, 0x130, 0xf, 0xf, false); // wave_shl:1
-        const bool ev1 = l < 63 && ((im >> (l + 1)) & 1);
-        const bool no_impr = best >= 258 || cn1 == 0 || (ev1 && !(en >> 31) && (en & 511) <= best);
-        const bool impr = best < 258 && ev1 && !(en >> 31) && (en & 511) > best;
-        g.stop = ballot(ev ? (usable || cut) : cn != 0);
-        g.fast = ballot(ev && usable && !cut && no_impr);
-        g.impr = ballot(ev && usable && !cut && impr);
-        g.cut = ballot(ev && cut);
+        const uint64_t imv = im >> l;
+        uint32_t ev = (uint32_t)imv & 1u, ev1 = (uint32_t)(imv >> 1) & 1u; // (lane 63: im >> 64 is 0)
+        const uint32_t ge4 = neg(3u - best), eq3 = neg((best ^ 3u) - 1u), near = neg(x - bq - 4097u);
+        uint32_t usable = ge4 | (eq3 & near);                                // TOO_FAR
+        const uint32_t enb = en & 511u, enc = en >> 31, le = neg(best - enb) ^ 1u, ge258 = neg(257u - best);
+        const uint32_t cn1z = neg(cn1 - 1u), cnnz = neg(cn - 1u) ^ 1u;
+        asm volatile("" : "+v"(ev), "+v"(ev1), "+v"(usable), "+v"(cutc)); // (keep them integers)
+        const uint32_t no_impr = ge258 | cn1z | (ev1 & (enc ^ 1u) & le);
+        const uint32_t impr = (ge258 ^ 1u) & ev1 & (enc ^ 1u) & (le ^ 1u);
+        const uint32_t okfast = ev & usable & (cutc ^ 1u);
+        g.stop = ballot(((ev & (usable | cutc)) | ((ev ^ 1u) & cnnz)) != 0u);
+        g.fast = ballot((okfast & no_impr) != 0u);
+        g.impr = ballot((okfast & impr) != 0u);
+        g.cut = ballot((ev & cutc) != 0u);
     }
     // Token sink: tokens collect in one VGPR (lane k holds token 64 * block + k) and leave
     // with one coalesced store per 64 tokens, so emitting costs no exec-masked stores.
@@ -871,12 +880,20 @@ struct SmallWave {
     };
     __device__ void tb_flush(TokBuf &t) { tok[t.n - 64 + (uint32_t)lane_id()] = t.v; }
     __device__ void tb_put(TokBuf &t, uint32_t x) {
+#ifdef PMC_DIAG_NOTOK // diagnostic: count tokens only (output invalid; measures emission cost)
+        t.n++;
+        return;
+#endif
         t.v = (uint32_t)lane_id() == (t.n & 63) ? x : t.v;
         t.n++;
         if ((t.n & 63) == 0) tb_flush(t);
     }
     // literal tokens for positions p .. p + cnt - 1
     __device__ void tb_run(TokBuf &t, uint32_t p, uint32_t cnt) {
+#ifdef PMC_DIAG_NOTOK
+        t.n += cnt;
+        return;
+#endif
         const uint32_t l = (uint32_t)lane_id();
         while (cnt) {
             count(7);
@@ -929,6 +946,9 @@ struct SmallWave {
         TokBuf tb;
         uint32_t i = 0, ml = 2, ms = 0, av = 0;
         uint32_t hci = 0;              // HC word cached in SGPRs
+#if defined(PMC_DIAG_SALU) || defined(PMC_DIAG_VALU)
+        uint32_t diag_s = 0, diag_s1 = 1, diag_s2 = 2, diag_s3 = 3, diag_v = 0, diag_v1 = 1, diag_v2 = 2, diag_v3 = 3;
+#endif
         uint64_t hcw = rfl64(HC[0]);
         while (i < len) {
             // (the parse state is wave-uniform: keep it in SGPRs so control stays scalar)
@@ -938,6 +958,27 @@ struct SmallWave {
             av = rfl(av);
             tb.n = rfl(tb.n);
             count(14);
+#ifdef PMC_DIAG_SALU // diagnostic builds only: extra scalar / vector work per parse step
+            // (s_mov_b32 / v_mov_b32 on independent registers: no SCC or VCC side effects)
+            asm volatile("s_mov_b32 %0, %1\n s_mov_b32 %1, %2\n s_mov_b32 %2, %3\n s_mov_b32 %3, %0\n"
+                         "s_mov_b32 %0, %1\n s_mov_b32 %1, %2\n s_mov_b32 %2, %3\n s_mov_b32 %3, %0\n"
+                         "s_mov_b32 %0, %1\n s_mov_b32 %1, %2\n s_mov_b32 %2, %3\n s_mov_b32 %3, %0\n"
+                         "s_mov_b32 %0, %1\n s_mov_b32 %1, %2\n s_mov_b32 %2, %3\n s_mov_b32 %3, %0\n"
+                         "s_mov_b32 %0, %1\n s_mov_b32 %1, %2\n s_mov_b32 %2, %3\n s_mov_b32 %3, %0\n"
+                         : "+s"(diag_s), "+s"(diag_s1), "+s"(diag_s2), "+s"(diag_s3));
+#endif
+#ifdef PMC_DIAG_NOP
+            asm volatile("s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n"
+                         "s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n");
+#endif
+#ifdef PMC_DIAG_VALU
+            asm volatile("v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
+                         "v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
+                         "v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
+                         "v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
+                         "v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
+                         : "+v"(diag_v), "+v"(diag_v1), "+v"(diag_v2), "+v"(diag_v3));
+#endif
             if (ml == 2) {
                 // no pending match: positions without chain candidates only pass the pending
                 // literal on, so jump to the next position that has candidates
@@ -1055,6 +1096,10 @@ struct SmallWave {
             }
         }
         if (av) tb_put(tb, i - 1);
+#if defined(PMC_DIAG_SALU) || defined(PMC_DIAG_VALU)
+        if (rfl(diag_s + diag_s1 + diag_s2 + diag_s3 + diag_v + diag_v1 + diag_v2 + diag_v3) == 0xdeadbeefu)
+            tb_put(tb, 0); // (keeps the diagnostic work alive)
+#endif
         tb_finish(tb);
         wave_sync_global();
         return rfl(tb.n);
