@@ -827,18 +827,29 @@ struct SmallWave {
         q = v ? q : 0u;
         load16(q, B0, B1);
         const uint32_t nice = (len - P) < 258 ? (len - P) : 258;
+        // (branch-free on the vector ALU: 0/1 integers and products instead of bools and
+        // selects, which became exec-mask and lane-mask work on the saturated scalar unit)
+        auto eq16 = [](uint64_t z0, uint64_t z1) { // equal leading bytes of 16 (16 when equal)
+            const uint32_t c0 = eq_bytes8(z0);
+            return c0 + (c0 >> 3) * eq_bytes8(z1);
+        };
+        auto is0 = [](uint64_t z0, uint64_t z1) { // 1 iff both words are zero
+            const uint32_t t = (uint32_t)z0 | (uint32_t)(z0 >> 32) | (uint32_t)z1 | (uint32_t)(z1 >> 32);
+            return 1u >> (t < 1u ? t : 1u);
+        };
         const uint64_t y0 = A0 ^ B0, y1 = A1 ^ B1;
-        uint32_t cl = y0 ? eq_bytes8(y0) : 8u + eq_bytes8(y1);
-        bool ext = v && (y0 | y1) == 0 && nice > 16;
+        uint32_t cl = eq16(y0, y1);
+        uint32_t ext = (v ? 1u : 0u) & is0(y0, y1) & ((16u - nice) >> 31);
+        asm volatile("" : "+v"(ext));
         uint32_t off = 16;
-        while (ballot(ext)) {
+        while (ballot(ext != 0u)) {
             count(8);
             uint64_t C0, C1, D0, D1;
-            load16(ext ? P + off : 0u, C0, C1);
-            load16(ext ? q + off : 0u, D0, D1);
+            load16((P + off) * ext, C0, C1);
+            load16((q + off) * ext, D0, D1);
             const uint64_t z0 = C0 ^ D0, z1 = C1 ^ D1;
-            cl = ext ? off + (z0 ? eq_bytes8(z0) : 8u + eq_bytes8(z1)) : cl;
-            ext = ext && (z0 | z1) == 0 && off + 16 < nice;
+            cl += ext * (off + eq16(z0, z1) - cl);
+            ext &= is0(z0, z1) & ((off + 16u - nice) >> 31);
             off += 16;
         }
         cl = cl < nice ? cl : nice;
