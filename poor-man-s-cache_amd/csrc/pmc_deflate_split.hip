@@ -135,10 +135,46 @@ struct LaneTrees {
         return kind == 1 ? 5u : x < 144 ? 8u : x < 256 ? 9u : x < 280 ? 7u : 8u;
     }
     template <class Freq>
-    __device__ int build(Freq freq, int elems, uint32_t row0, int kind, int max_length, int64_t &opt, int64_t &stat) {
+    __device__ int build(Freq freq, int elems, uint32_t row0, int kind, int max_length, int64_t &opt, int64_t &stat,
+                         PMC_GLB const uint16_t *grow = nullptr) {
         int heap_len = 0, max_code = -1;
+        if (grow) {
+            // frequencies from a 16-byte aligned global row: 32 per batch in four 16-byte loads, the
+            // next batch in flight while this one is inserted (HBM latency was paid per 8 values)
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            PMC_GLB const v4u *g4 = (PMC_GLB const v4u *)grow;
+            const int nb = (elems + 31) / 32;
+            v4u cur[4], nxt[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) cur[i] = i * 8 < elems ? g4[i] : v4u{0, 0, 0, 0};
+            for (int b = 0; b < nb; b++) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int q = (b + 1) * 4 + i;
+                    nxt[i] = b + 1 < nb && q * 8 < elems ? g4[q] : v4u{0, 0, 0, 0};
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+#pragma unroll
+                    for (int h = 0; h < 8; h++) {
+                        const int nn = b * 32 + i * 8 + h;
+                        const uint32_t f = nn < elems ? (cur[i][h >> 1] >> (16 * (h & 1))) & 0xffffu : 0u;
+                        if (f) {
+                            if (heap_len == CAP) {
+                                deferred = true;
+                                return -1;
+                            }
+                            setH(++heap_len, f << 15 | (uint32_t)nn);
+                            max_code = nn;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) cur[i] = nxt[i];
+            }
+        }
         // (frequencies fetched 8 at a time so the loads overlap)
-        for (int n0 = 0; n0 < elems; n0 += 8) {
+        for (int n0 = 0; !grow && n0 < elems; n0 += 8) {
             uint32_t f8[8];
 #pragma unroll
             for (int k = 0; k < 8; k++) f8[k] = n0 + k < elems ? freq(n0 + k) : 0u;
@@ -290,7 +326,7 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC
     for (uint32_t s = 0; s < kSplitRows; s += 16) *reinterpret_cast<uint4 *>(t.lens + s) = make_uint4(0, 0, 0, 0);
     int64_t opt = 0, stat = 0;
     auto hist = [&](int s) -> uint32_t { return t.hist[s]; };
-    const int l_max = t.build(hist, kLCodes, 0, 0, kMaxBits, opt, stat);
+    const int l_max = t.build(hist, kLCodes, 0, 0, kMaxBits, opt, stat, (PMC_GLB const uint16_t *)t.hist);
     if (t.deferred) {
         a.cP[v] = kPlanDeferred;
         a.cD[atomicAdd(a.cD + a.count, 1u)] = (uint32_t)v;
