@@ -80,6 +80,11 @@ int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *
                               const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
                               const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
                               void *stream);
+/* crc[i] = CRC-32 (the gzip trailer's, zlib crc32.c) of buf[off[i] .. off[i] + len[i]), all
+ * device-resident; the engine of decompression's CRC check, exported for callers that verify
+ * stored members themselves.  Stream-ordered like the batch calls above. */
+int pmc_crc32_batch(pmc_ctx *ctx, const uint8_t *buf, const uint64_t *off, const uint32_t *len,
+                    uint32_t n, uint32_t *crc, void *stream);
 /* isize[i] = ISIZE trailer of member i (0 if src_len[i] < 18). */
 int pmc_gzip_isize_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
                          const uint32_t *src_len, uint32_t n, uint32_t *isize, void *stream);

@@ -27,6 +27,9 @@ __constant__ Tables c_tables = make_tables();
 __constant__ uint32_t c_crc_table[256];
 __constant__ uint32_t c_crc_shift16[kCrcShiftEntries];
 __constant__ uint32_t c_crc_shift64k[kCrcShiftEntries];
+__constant__ uint32_t c_crc_slice8[8 * 256];
+__constant__ uint32_t c_crc_zpiece[4 * 4 * 256];
+__constant__ uint32_t c_crc_ones[kCrcQuarterMax + 1];
 
 static thread_local std::string g_err;
 static void set_err(const char *what, hipError_t e) {
@@ -86,6 +89,20 @@ static int upload_constants() {
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_table), tab, sizeof tab));
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_shift16), s16, sizeof s16));
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_shift64k), s64k, sizeof s64k));
+    static uint32_t s8[8 * 256], zp[4 * 4 * 256], ones[kCrcQuarterMax + 1];
+    for (int b = 0; b < 256; b++) {
+        s8[b] = tab[b];
+        for (int k = 1; k < 8; k++) s8[k * 256 + b] = (s8[(k - 1) * 256 + b] >> 8) ^ tab[s8[(k - 1) * 256 + b] & 0xff];
+    }
+    for (int k = 0; k < 4; k++) {
+        const uint32_t m = h_x2nmodp(1, 9 + k); // x^(8 * 64 * 2^k)
+        for (int j = 0; j < 4; j++)
+            for (int b = 0; b < 256; b++) zp[(k * 4 + j) * 256 + b] = h_multmodp(m, (uint32_t)b << (8 * j));
+    }
+    for (uint32_t len = 0; len <= kCrcQuarterMax; len++) ones[len] = h_multmodp(h_x2nmodp(len, 3), 0xFFFFFFFFu);
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_slice8), s8, sizeof s8));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_zpiece), zp, sizeof zp));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_ones), ones, sizeof ones));
     return PMC_OK;
 }
 
@@ -524,9 +541,9 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
         const unsigned lb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * 16);
         klaunch(ctx, PMC_K_INFLATE_LANE, st,
                 [&] { hipLaunchKernelGGL(inflate_lane_kernel, dim3(lb), dim3(64), kLaneLdsBytes, st, a); });
-        const unsigned vb = (unsigned)std::min<uint64_t>(((uint64_t)n + 255) / 256, (uint64_t)ctx->cus * 8);
+        const unsigned vb = (unsigned)std::min<uint64_t>(((uint64_t)n + 511) / 512, (uint64_t)ctx->cus * 4);
         klaunch(ctx, PMC_K_INFLATE_VERIFY, st,
-                [&] { hipLaunchKernelGGL(inflate_verify_kernel, dim3(vb), dim3(256), 0, st, a); });
+                [&] { hipLaunchKernelGGL(inflate_verify_kernel, dim3(vb), dim3(512), 0, st, a); });
         a.retry_only = 1;
         a.order = nullptr;
     }
@@ -589,6 +606,15 @@ PMC_API int pmc_ctx_kernel_times(pmc_ctx *ctx, double *ms, uint32_t *launches, i
     }
     ctx->krecs.clear();
     return rc;
+}
+
+PMC_API int pmc_crc32_batch(pmc_ctx *ctx, const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint32_t n,
+                            uint32_t *crc, void *stream) {
+    if (!ctx || (n && (!buf || !off || !len || !crc))) return PMC_E_ARG;
+    if (!n) return PMC_OK;
+    const unsigned b = (unsigned)std::min<uint64_t>(((uint64_t)n + 511) / 512, (uint64_t)ctx->cus * 4);
+    hipLaunchKernelGGL(crc32_batch_kernel, dim3(b), dim3(512), 0, (hipStream_t)stream, buf, off, len, (uint64_t)n, crc);
+    return hipGetLastError() == hipSuccess ? PMC_OK : PMC_E_NO_DEVICE;
 }
 
 PMC_API int pmc_gzip_isize_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,

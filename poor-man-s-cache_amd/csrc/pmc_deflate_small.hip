@@ -274,7 +274,6 @@ struct TreeOut {
     int dummy[2]; // symbols whose freq build_tree set to 1 (zlib's "at least 2 codes"), or -1
 };
 
-#define PMC_GLB __attribute__((address_space(1)))
 // chain candidates evaluated per position by the on-demand parse's wave step (the rest, when
 // needed, by search()); at most 32 (5-bit field in the eval key)
 #ifndef PMC_PRECAND

@@ -16,6 +16,8 @@ constexpr int kWave = 64;
 // LDS-typed pointers: accesses compile to ds_* with 32-bit addresses wherever the pointer
 // itself lives (a generic pointer kept in a struct in scratch degrades to flat_* ops).
 #define PMC_LDS __attribute__((address_space(3)))
+// global-typed pointers: global_* loads (vmcnt only) instead of flat_* (vmcnt + lgkmcnt)
+#define PMC_GLB __attribute__((address_space(1)))
 template <class T>
 __device__ __forceinline__ PMC_LDS T *to_lds(void *p) {
     return (PMC_LDS T *)(p);
@@ -34,6 +36,13 @@ extern __constant__ Tables c_tables;
 extern __constant__ uint32_t c_crc_table[256];
 extern __constant__ uint32_t c_crc_shift16[kCrcShiftEntries];  // x^(8*16*d)   mod P
 extern __constant__ uint32_t c_crc_shift64k[kCrcShiftEntries]; // x^(8*65536*d) mod P
+// quarter-wave CRC (wave_crc32_members): a member of up to kCrcQuarterMax bytes takes 16
+// lanes, each lane one kCrcPiece-byte piece
+constexpr uint32_t kCrcPiece = 64;
+constexpr uint32_t kCrcQuarterMax = 16 * kCrcPiece;
+extern __constant__ uint32_t c_crc_slice8[8 * 256];              // slicing-by-8: T_k = byte then k zero bytes
+extern __constant__ uint32_t c_crc_zpiece[4 * 4 * 256];          // [level k][byte j][b]: (b << 8j) x^(8*64*2^k)
+extern __constant__ uint32_t c_crc_ones[kCrcQuarterMax + 1];     // 0xFFFFFFFF x^(8*len): the init's share
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }

@@ -653,25 +653,131 @@ __global__ void __launch_bounds__(256) order_scatter_kernel(const uint32_t *src_
     for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) order[atomicAdd(&h[order_bin(src_len[i])], 1u)] = (uint32_t)i;
 }
 
-// CRC-32 of every member the lane kernel decoded (wave per member); a mismatch sends the
-// member to the wave kernel for zlib's verdict.
-__global__ void __launch_bounds__(256) inflate_verify_kernel(InflateArgs a) {
-    __shared__ uint32_t crc_tab[256];
-    for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
+// CRC-32 of the members g + j (j in `todo`) of a batch of byte strings, returned in lane j.
+// Members of up to kCrcQuarterMax bytes go four to a wave: quarter q (16 lanes) takes the
+// q-th member of the round, lane s of it the s-th 64-byte piece counted from the member's
+// END, front-padded with zero bytes.  A piece runs slicing-by-8 from register 0 (17 dword
+// loads, v_alignbyte for the member's byte alignment); the quarter then folds its pieces in
+// four DPP row_shl levels, shifting the earlier half past 64*2^k bytes with a 4x256 table,
+// and the init value's share 0xFFFFFFFF x^(8 len) comes from c_crc_ones (zeros in front of
+// a register-0 CRC leave it unchanged, so the padding is free).  Longer members take the
+// whole wave (wave_crc32).  `mylen` is lane j's member length.
+__device__ __forceinline__ uint32_t crc_piece64(const uint8_t *buf, uint64_t off, uint32_t len, uint32_t s,
+                                                PMC_LDS const uint32_t *s8) {
+    const int64_t pend = (int64_t)len - (int64_t)kCrcPiece * s, pbeg = pend - kCrcPiece;
+    const uint64_t base = (uint64_t)buf + off;
+    const uint64_t lo = base & ~(uint64_t)3, hi = (base + len - 1) & ~(uint64_t)3;
+    const uint64_t ab = (uint64_t)((int64_t)base + pbeg) & ~(uint64_t)3;
+    const uint32_t sh = (uint32_t)(base + (uint64_t)pend) & 3;
+    const int32_t lead = pbeg < 0 ? (int32_t)-pbeg : 0;
+    uint32_t w[17];
+#pragma unroll
+    for (int i = 0; i < 17; i++) {
+        uint64_t p = ab + 4 * i;
+        p = p < lo ? lo : p;
+        p = p > hi ? hi : p;
+        w[i] = *(const PMC_GLB uint32_t *)p;
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        uint32_t x[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int i = 2 * k + h;
+            uint32_t v = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+            const int32_t r = lead - 4 * i;
+            v = r <= 0 ? v : (r >= 4 ? 0u : v & (0xFFFFFFFFu << (8 * r)));
+            x[h] = v;
+        }
+        const uint32_t a0 = x[0] ^ c, a1 = x[1];
+        c = s8[7 * 256 + (a0 & 0xff)] ^ s8[6 * 256 + ((a0 >> 8) & 0xff)] ^ s8[5 * 256 + ((a0 >> 16) & 0xff)] ^
+            s8[4 * 256 + (a0 >> 24)] ^ s8[3 * 256 + (a1 & 0xff)] ^ s8[2 * 256 + ((a1 >> 8) & 0xff)] ^
+            s8[1 * 256 + ((a1 >> 16) & 0xff)] ^ s8[a1 >> 24];
+    }
+    return c;
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t crc_fold_level(uint32_t v, PMC_LDS const uint32_t *zp) {
+    const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + (1 << K), 0xf, 0xf, false);
+    PMC_LDS const uint32_t *z = zp + K * 1024;
+    return v ^ z[t & 0xff] ^ z[256 + ((t >> 8) & 0xff)] ^ z[512 + ((t >> 16) & 0xff)] ^ z[768 + (t >> 24)];
+}
+
+__device__ uint32_t wave_crc32_members(const uint8_t *buf, const uint64_t *off, uint64_t g, uint64_t todo,
+                                       uint32_t mylen, PMC_LDS const uint32_t *s8, PMC_LDS const uint32_t *zp) {
+    const int l = lane_id(), q = l >> 4, s = l & 15;
+    uint32_t res = 0;
+    uint64_t small = todo & ballot(mylen <= kCrcQuarterMax);
+    uint64_t large = todo & ~small;
+    while (small) {
+        int jq[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            jq[t] = small ? __builtin_ctzll(small) : 64;
+            small &= small - 1;
+        }
+        const int j = q == 0 ? jq[0] : q == 1 ? jq[1] : q == 2 ? jq[2] : jq[3];
+        const uint32_t len = (uint32_t)__shfl((int)mylen, j & 63);
+        uint32_t c = 0;
+        if (j < 64 && kCrcPiece * (uint32_t)s < len) c = crc_piece64(buf, off[g + (uint64_t)j], len, (uint32_t)s, s8);
+        c = crc_fold_level<0>(c, zp);
+        c = crc_fold_level<1>(c, zp);
+        c = crc_fold_level<2>(c, zp);
+        c = crc_fold_level<3>(c, zp);
+        c = ~(c ^ c_crc_ones[len <= kCrcQuarterMax ? len : 0]);
+        const int src = l == jq[0] ? 0 : l == jq[1] ? 16 : l == jq[2] ? 32 : l == jq[3] ? 48 : -1;
+        const uint32_t mine = (uint32_t)__shfl((int)c, src & 63);
+        res = src >= 0 ? mine : res;
+    }
+    while (large) {
+        const int j = __builtin_ctzll(large);
+        large &= large - 1;
+        const uint32_t len = (uint32_t)__shfl((int)mylen, j);
+        const uint32_t c = wave_crc32(buf + off[g + (uint64_t)j], len, s8);
+        res = l == j ? c : res;
+    }
+    return res;
+}
+
+__device__ __forceinline__ void load_crc_tables(PMC_LDS uint32_t *s8, PMC_LDS uint32_t *zp) {
+    for (int k = threadIdx.x; k < 8 * 256; k += blockDim.x) s8[k] = c_crc_slice8[k];
+    for (int k = threadIdx.x; k < 4 * 4 * 256; k += blockDim.x) zp[k] = c_crc_zpiece[k];
     __syncthreads();
+}
+
+// CRC-32 of every member the lane kernel decoded; a mismatch sends the member to the wave
+// kernel for zlib's verdict.
+__global__ void __launch_bounds__(512) inflate_verify_kernel(InflateArgs a) {
+    __shared__ uint32_t s8[8 * 256], zp[4 * 4 * 256];
+    load_crc_tables(to_lds<uint32_t>(s8), to_lds<uint32_t>(zp));
     const int wpb = blockDim.x / 64, l = lane_id();
     const uint64_t wave = (uint64_t)blockIdx.x * wpb + threadIdx.x / 64, nwaves = (uint64_t)gridDim.x * wpb;
     for (uint64_t g = wave * 64; g < a.n; g += nwaves * 64) {
         const uint64_t vl = g + (uint64_t)l;
-        const int32_t myrc = vl < a.n ? a.rc[vl] : -1;
-        uint64_t todo = ballot(vl < a.n && myrc == 0);
-        while (todo) {
-            const int j = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const uint64_t v = g + (uint64_t)j;
-            const uint32_t c = wave_crc32(a.dst + a.dst_off[v], a.dst_len[v], to_lds<const uint32_t>(crc_tab));
-            if (l == 0 && c != a.crc_expect[v]) a.rc[v] = kInflateRetry;
-        }
+        const bool ok = vl < a.n && a.rc[vl] == 0;
+        const uint32_t mylen = ok ? a.dst_len[vl] : 0;
+        const uint32_t c = wave_crc32_members(a.dst, a.dst_off, g, ballot(ok), mylen, to_lds<const uint32_t>(s8),
+                                              to_lds<const uint32_t>(zp));
+        if (ok && c != a.crc_expect[vl]) a.rc[vl] = kInflateRetry;
+    }
+}
+
+// crc[i] = CRC-32 (gzip trailer) of buf[off[i] .. off[i] + len[i]) -- the verify pass's
+// engine as a batch entry point
+__global__ void __launch_bounds__(512) crc32_batch_kernel(const uint8_t *buf, const uint64_t *off, const uint32_t *len,
+                                                          uint64_t n, uint32_t *crc) {
+    __shared__ uint32_t s8[8 * 256], zp[4 * 4 * 256];
+    load_crc_tables(to_lds<uint32_t>(s8), to_lds<uint32_t>(zp));
+    const int wpb = blockDim.x / 64, l = lane_id();
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + threadIdx.x / 64, nwaves = (uint64_t)gridDim.x * wpb;
+    for (uint64_t g = wave * 64; g < n; g += nwaves * 64) {
+        const uint64_t vl = g + (uint64_t)l;
+        const bool ok = vl < n;
+        const uint32_t c = wave_crc32_members(buf, off, g, ballot(ok), ok ? len[vl] : 0, to_lds<const uint32_t>(s8),
+                                              to_lds<const uint32_t>(zp));
+        if (ok) crc[vl] = c;
     }
 }
 

@@ -111,5 +111,7 @@ template <bool kHbm>
 __global__ void inflate_kernel(InflateArgs a);
 __global__ void inflate_lane_kernel(InflateArgs a);
 __global__ void inflate_verify_kernel(InflateArgs a);
+__global__ void crc32_batch_kernel(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint64_t n,
+                                   uint32_t *crc);
 
 } // namespace pmc

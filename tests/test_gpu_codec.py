@@ -297,3 +297,32 @@ def test_host_batch_api(ctx, golden):
     back = ctx.decompress_many([gz for _, gz in out])
     for (rc, r), v in zip(back, vals):
         assert rc == 0 and r == v
+
+
+def test_crc32_batch_vs_oracle(ctx, D):
+    """pmc_crc32_batch (the engine of decompression's CRC check: quarter-wave slicing-by-8 for
+    members <= 1 KiB, whole wave above) vs the oracle's zlib crc32 on ragged lengths and every
+    byte alignment, first member at the buffer's start and last one ending at its end."""
+    import torch
+    import pmc_codec
+    from oracle import pyoracle as O
+    rng = np.random.default_rng(0xC3C)
+    lens = np.concatenate([np.arange(0, 1100), rng.integers(0, 1025, 1500), rng.integers(1025, 9000, 300),
+                           [1024, 1023, 1025, 64, 63, 65, 2048, 65536 + 17]]).astype(np.int64)
+    rng.shuffle(lens)
+    gaps = rng.integers(0, 8, len(lens))
+    gaps[0] = 0
+    offs = np.cumsum(gaps + np.concatenate([[0], lens[:-1]]))
+    total = int(offs[-1] + lens[-1])
+    buf = rng.integers(0, 256, total, dtype=np.uint8)
+    dbuf = torch.from_numpy(buf).cuda()
+    doff = torch.from_numpy(offs.astype(np.uint64).view(np.int64)).cuda()
+    dlen = torch.from_numpy(lens.astype(np.int32)).cuda()
+    crc = torch.full((len(lens),), -1, dtype=torch.int32, device="cuda")
+    assert pmc_codec.lib().pmc_crc32_batch(ctx.handle, dbuf.data_ptr(), doff.data_ptr(), dlen.data_ptr(), len(lens),
+                                           crc.data_ptr(), D.stream_handle()) == 0
+    sync()
+    got = crc.cpu().numpy().view(np.uint32)
+    raw = buf.tobytes()
+    bad = [i for i in range(len(lens)) if got[i] != O.crc32(raw[offs[i]:offs[i] + lens[i]])]
+    assert not bad, [(int(lens[i]), int(offs[i]) % 4) for i in bad[:10]]
