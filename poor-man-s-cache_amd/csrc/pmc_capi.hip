@@ -178,6 +178,15 @@ struct pmc_ctx {
     DevBuf staging;              // device side of host-API calls
     uint64_t *dbg = nullptr;     // diagnostic stamp sums (PMC_STAMPS builds)
     HostBuf pinned;              // host side of host-API calls
+    // pmc_gzip_*_batch_pinned: chunk c's H2D (stream h2d), kernels (stream) and D2H (stream d2h)
+    // overlap those of chunks c +- 1; slot c & 1 of `pipe` holds chunk c's arrays and bytes.
+    struct Pipe {
+        hipStream_t h2d = nullptr, d2h = nullptr;
+        hipEvent_t in[2] = {}, out[2] = {}, done[2] = {};
+        DevBuf slot[2];
+        HostBuf total;           // packed mode: each slot's chunk total, read by the host
+        bool busy[2] = {false, false};
+    } pipe;
 };
 
 namespace {
@@ -316,6 +325,18 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     c->krecs.clear();
     c->staging.release();
     c->pinned.release();
+    if (c->pipe.h2d) {
+        (void)hipStreamSynchronize(c->pipe.d2h);
+        for (int k = 0; k < 2; k++) {
+            (void)hipEventDestroy(c->pipe.in[k]);
+            (void)hipEventDestroy(c->pipe.out[k]);
+            (void)hipEventDestroy(c->pipe.done[k]);
+            c->pipe.slot[k].release();
+        }
+        c->pipe.total.release();
+        (void)hipStreamDestroy(c->pipe.h2d);
+        (void)hipStreamDestroy(c->pipe.d2h);
+    }
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -700,6 +721,216 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     }
     return PMC_OK;
 }
+
+// Rebases one chunk's offsets onto its device copy: src_off -= sb, dst_off -= db (dst_off may be null).
+__global__ void rebase_kernel(uint64_t *soff, uint64_t *doff, uint32_t n, uint64_t sb, uint64_t db) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        soff[i] -= sb;
+        if (doff) doff[i] -= db;
+    }
+}
+
+// Exclusive prefix sum of v[i] (0 where rc[i] != 0, if rc is given) into out[]; kScanBlock values per
+// block, block totals to bsum[] (scan_blocks_kernel turns them into block bases, bsum[nb] = total).
+constexpr uint32_t kScanBlock = 1024;
+__global__ __launch_bounds__(kScanBlock) void scan_local_kernel(const uint32_t *v, const int32_t *rc, uint32_t n,
+                                                                 uint64_t *out, uint64_t *bsum) {
+    __shared__ uint64_t s[kScanBlock];
+    const uint32_t t = threadIdx.x, i = blockIdx.x * kScanBlock + t;
+    const uint64_t x = i < n && !(rc && rc[i] != 0) ? v[i] : 0;
+    s[t] = x;
+    __syncthreads();
+    for (uint32_t d = 1; d < kScanBlock; d <<= 1) {
+        uint64_t y = t >= d ? s[t - d] : 0;
+        __syncthreads();
+        s[t] += y;
+        __syncthreads();
+    }
+    if (i < n) out[i] = s[t] - x;
+    if (t == kScanBlock - 1) bsum[blockIdx.x] = s[t];
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_blocks_kernel(uint64_t *bsum, uint32_t nb) {
+    __shared__ uint64_t s[kScanBlock];
+    __shared__ uint64_t carry;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nb; base += kScanBlock) {
+        const uint64_t x = base + t < nb ? bsum[base + t] : 0;
+        s[t] = x;
+        __syncthreads();
+        for (uint32_t d = 1; d < kScanBlock; d <<= 1) {
+            uint64_t y = t >= d ? s[t - d] : 0;
+            __syncthreads();
+            s[t] += y;
+            __syncthreads();
+        }
+        if (base + t < nb) bsum[base + t] = carry + s[t] - x;
+        __syncthreads();
+        if (t == kScanBlock - 1) carry += s[t];
+        __syncthreads();
+    }
+    if (t == 0) bsum[nb] = carry;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_add_kernel(uint64_t *out, uint32_t n, const uint64_t *bsum) {
+    const uint32_t i = blockIdx.x * kScanBlock + threadIdx.x;
+    if (i < n) out[i] += bsum[blockIdx.x];
+}
+
+// One wave per member: slot bytes dst[doff[i] ..+ len[i]) -> packed[poff[i] ..) (rc[i] != 0: none).
+__global__ __launch_bounds__(256) void compact_kernel(const uint8_t *dst, const uint64_t *doff, const uint32_t *len,
+                                                      const int32_t *rc, const uint64_t *poff, uint32_t n,
+                                                      uint8_t *packed) {
+    const uint32_t lane = threadIdx.x & 63, waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += waves) {
+        if (rc[i] != 0) continue;
+        const uint8_t *a = dst + doff[i];
+        uint8_t *b = packed + poff[i];
+        for (uint32_t k = lane; k < len[i]; k += 64) b[k] = a[k];
+    }
+}
+
+int scan_u32(const uint32_t *v, const int32_t *rc, uint32_t n, uint64_t *out, uint64_t *bsum, hipStream_t st) {
+    const uint32_t nb = (n + kScanBlock - 1) / kScanBlock;
+    hipLaunchKernelGGL(scan_local_kernel, dim3(nb), dim3(kScanBlock), 0, st, v, rc, n, out, bsum);
+    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(kScanBlock), 0, st, bsum, nb);
+    hipLaunchKernelGGL(scan_add_kernel, dim3(nb), dim3(kScanBlock), 0, st, out, n, bsum);
+    HIP_TRY(hipGetLastError());
+    return PMC_OK;
+}
+
+int pipe_init(pmc_ctx *ctx) {
+    auto &P = ctx->pipe;
+    if (P.h2d) return PMC_OK;
+    HIP_TRY(hipStreamCreateWithFlags(&P.h2d, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&P.d2h, hipStreamNonBlocking));
+    for (int k = 0; k < 2; k++) {
+        HIP_TRY(hipEventCreateWithFlags(&P.in[k], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&P.out[k], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&P.done[k], hipEventDisableTiming));
+    }
+    return P.total.ensure(64);
+}
+
+// Pinned host batch, chunked and software-pipelined over three streams (s = c & 1):
+//   h2d:    offsets/lengths/caps of chunk c, then its source byte range  -> event in[s]
+//   stream: rebase offsets, the codec kernels                            -> event out[s]
+//   d2h:    dst_len, rc, then the chunk's destination bytes              -> event done[s]
+// and chunk c + 2 reuses slot s after done[s].  Chunk c's source bytes are the range
+// [min src_off, max src_off + src_len) of its values (packed layouts copy exactly their bytes).
+// Slot mode (dst_off given): the destination range [min dst_off, max dst_off + dst_cap) is copied
+// back whole.  Packed mode (dst_off null): the device lays the chunk's slots out by a scan of
+// dst_cap, compacts the results by a scan of dst_len (rc != 0 -> 0 bytes) and copies back only
+// those bytes, appended to dst; the host waits for chunk c's total (on the compute stream, after
+// its kernels) only once chunk c + 1's kernels are enqueued, so the device never idles on it.
+int pinned_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                 uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+                 int32_t *rc, uint32_t max_len, uint32_t chunk) {
+    if (!ctx || !src || !src_off || !src_len || !dst || !dst_cap || !dst_len || !rc) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    int r = pipe_init(ctx);
+    if (r) return r;
+    auto &P = ctx->pipe;
+    const bool packed = dst_off == nullptr;
+    if (chunk == 0) chunk = std::max<uint32_t>(65536, (n + 15) / 16);
+    auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    const uint32_t nchunks = (uint32_t)((n + (uint64_t)chunk - 1) / chunk);
+    volatile uint64_t *h_total = (volatile uint64_t *)P.total.p;  // chunk totals, slot s at [s]
+    uint8_t *d_pk[2] = {nullptr, nullptr};
+    uint64_t out_pos = 0;
+    // packed mode: chunk c's bytes go back once its total is known (called after chunk c + 1 is enqueued)
+    auto finish = [&](uint32_t c) -> int {
+        const uint32_t s = c & 1;
+        HIP_TRY(hipEventSynchronize(P.out[s]));
+        const uint64_t tot = h_total[s];
+        HIP_TRY(hipStreamWaitEvent(P.d2h, P.out[s], 0));
+        if (tot) HIP_TRY(hipMemcpyAsync(dst + out_pos, d_pk[s], tot, hipMemcpyDeviceToHost, P.d2h));
+        HIP_TRY(hipEventRecord(P.done[s], P.d2h));
+        out_pos += tot;
+        return PMC_OK;
+    };
+    for (uint32_t c = 0; c < nchunks; c++) {
+        const uint32_t a = c * chunk, m = std::min<uint32_t>(chunk, n - a), s = c & 1;
+        uint64_t sb = ~0ull, se = 0, db = ~0ull, de = 0;
+        for (uint32_t i = a; i < a + m; i++) {
+            sb = std::min(sb, src_off[i]);
+            se = std::max(se, src_off[i] + src_len[i]);
+        }
+        if (packed) {
+            db = 0;
+            for (uint32_t i = a; i < a + m; i++) de += dst_cap[i];
+        } else {
+            for (uint32_t i = a; i < a + m; i++) {
+                db = std::min(db, dst_off[i]);
+                de = std::max(de, dst_off[i] + dst_cap[i]);
+            }
+        }
+        const uint32_t nb = (m + kScanBlock - 1) / kScanBlock;
+        const uint64_t meta = al(m * 8ull) * 3 + al(m * 4ull) * 4 + al((nb + 1) * 8ull);
+        const uint64_t need = meta + al(se - sb + 16) + al(de - db + 16) * (packed ? 2 : 1);
+        if (need > P.slot[s].cap) {
+            // the slot's previous chunk must have drained before it is reallocated
+            if (P.busy[s]) HIP_TRY(hipEventSynchronize(P.done[s]));
+            r = P.slot[s].ensure(need + need / 8);
+            if (r) return r;
+            P.busy[s] = false;
+        }
+        uint8_t *dp = (uint8_t *)P.slot[s].p;
+        uint64_t *d_soff = (uint64_t *)dp, *d_doff = d_soff + al(m * 8ull) / 8, *d_poff = d_doff + al(m * 8ull) / 8;
+        uint32_t *d_slen = (uint32_t *)(d_poff + al(m * 8ull) / 8);
+        uint32_t *d_dcap = d_slen + al(m * 4ull) / 4, *d_dlen = d_dcap + al(m * 4ull) / 4;
+        int32_t *d_rc = (int32_t *)(d_dlen + al(m * 4ull) / 4);
+        uint64_t *d_bsum = (uint64_t *)(d_rc + al(m * 4ull) / 4);
+        uint8_t *d_src = dp + meta, *d_dst = d_src + al(se - sb + 16);
+        d_pk[s] = d_dst + al(de - db + 16);
+        if (P.busy[s]) HIP_TRY(hipStreamWaitEvent(P.h2d, P.done[s], 0));
+        HIP_TRY(hipMemcpyAsync(d_soff, src_off + a, m * 8ull, hipMemcpyHostToDevice, P.h2d));
+        if (!packed) HIP_TRY(hipMemcpyAsync(d_doff, dst_off + a, m * 8ull, hipMemcpyHostToDevice, P.h2d));
+        HIP_TRY(hipMemcpyAsync(d_slen, src_len + a, m * 4ull, hipMemcpyHostToDevice, P.h2d));
+        HIP_TRY(hipMemcpyAsync(d_dcap, dst_cap + a, m * 4ull, hipMemcpyHostToDevice, P.h2d));
+        HIP_TRY(hipMemcpyAsync(d_src, src + sb, se - sb, hipMemcpyHostToDevice, P.h2d));
+        HIP_TRY(hipEventRecord(P.in[s], P.h2d));
+        HIP_TRY(hipStreamWaitEvent(ctx->stream, P.in[s], 0));
+        hipLaunchKernelGGL(rebase_kernel, dim3(std::min<uint32_t>((m + 255) / 256, 1024)), dim3(256), 0, ctx->stream,
+                           d_soff, packed ? nullptr : d_doff, m, sb, db);
+        HIP_TRY(hipGetLastError());
+        if (packed && (r = scan_u32(d_dcap, nullptr, m, d_doff, d_bsum, ctx->stream))) return r;
+        r = dir == kCompress
+                ? pmc_gzip_compress_batch(ctx, d_src, d_soff, d_slen, m, d_dst, d_doff, d_dcap, d_dlen, d_rc,
+                                          max_len, ctx->stream)
+                : pmc_gzip_decompress_batch(ctx, d_src, d_soff, d_slen, m, d_dst, d_doff, d_dcap, d_dlen, d_rc,
+                                            max_len, ctx->stream);
+        if (r) return r;
+        if (packed) {
+            if ((r = scan_u32(d_dlen, d_rc, m, d_poff, d_bsum, ctx->stream))) return r;
+            hipLaunchKernelGGL(compact_kernel, dim3(std::min<uint32_t>((m + 3) / 4, 8192)), dim3(256), 0,
+                               ctx->stream, d_dst, d_doff, d_dlen, d_rc, d_poff, m, d_pk[s]);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipMemcpyAsync(dst_len + a, d_dlen, m * 4ull, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipMemcpyAsync(rc + a, d_rc, m * 4ull, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipMemcpyAsync((void *)(h_total + s), d_bsum + nb, 8, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipEventRecord(P.out[s], ctx->stream));
+            P.busy[s] = true;
+            if (c > 0 && (r = finish(c - 1))) return r;
+            continue;
+        }
+        HIP_TRY(hipEventRecord(P.out[s], ctx->stream));
+        HIP_TRY(hipStreamWaitEvent(P.d2h, P.out[s], 0));
+        HIP_TRY(hipMemcpyAsync(dst_len + a, d_dlen, m * 4ull, hipMemcpyDeviceToHost, P.d2h));
+        HIP_TRY(hipMemcpyAsync(rc + a, d_rc, m * 4ull, hipMemcpyDeviceToHost, P.d2h));
+        HIP_TRY(hipMemcpyAsync(dst + db, d_dst, de - db, hipMemcpyDeviceToHost, P.d2h));
+        HIP_TRY(hipEventRecord(P.done[s], P.d2h));
+        P.busy[s] = true;
+    }
+    if (packed && (r = finish(nchunks - 1))) return r;
+    HIP_TRY(hipStreamSynchronize(P.d2h));
+    P.busy[0] = P.busy[1] = false;
+    return PMC_OK;
+}
+
 } // namespace
 
 PMC_API int pmc_gzip_compress_batch_host(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
@@ -713,6 +944,22 @@ PMC_API int pmc_gzip_decompress_batch_host(pmc_ctx *ctx, const uint8_t *src, con
                                            const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
                                            int32_t *rc) {
     return host_batch(ctx, kDecompress, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc);
+}
+
+PMC_API int pmc_gzip_compress_batch_pinned(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                           const uint32_t *src_len, uint32_t n, uint8_t *dst,
+                                           const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+                                           int32_t *rc, uint32_t max_len, uint32_t chunk) {
+    return pinned_batch(ctx, kCompress, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len,
+                        chunk);
+}
+
+PMC_API int pmc_gzip_decompress_batch_pinned(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                             const uint32_t *src_len, uint32_t n, uint8_t *dst,
+                                             const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+                                             int32_t *rc, uint32_t max_len, uint32_t chunk) {
+    return pinned_batch(ctx, kDecompress, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len,
+                        chunk);
 }
 
 PMC_API int pmc_gzip_compress(pmc_ctx *ctx, const void *in, size_t in_len, void *out, size_t out_cap,

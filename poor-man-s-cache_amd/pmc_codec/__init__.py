@@ -58,6 +58,8 @@ SIGNATURES = {
     "pmc_crc32_batch": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p]),
     "pmc_gzip_compress_batch_host": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p]),
     "pmc_gzip_decompress_batch_host": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p]),
+    "pmc_gzip_compress_batch_pinned": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p, _u32, _u32]),
+    "pmc_gzip_decompress_batch_pinned": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p, _u32, _u32]),
     "pmc_gen_values": (_c.c_int, [_p, _u32, _u64, _c.c_int, _u64, _p, _u32, _u32, _p, _p]),
     "pmc_fill_layout": (_c.c_int, [_p, _p, _p, _u32, _u64, _u32, _u32, _p]),
     "pmc_compare_values": (_c.c_int, [_p, _p, _p, _p, _p, _p, _u32, _p, _p]),
@@ -199,6 +201,22 @@ class Context:
                                             max_len, stream)
         if r != 0:
             raise CodecUnavailable(f"pmc_gzip_decompress_batch = {r}: {last_error()}")
+
+    # ---------------- pinned host batches, pipelined over copy streams --------------
+    def compress_pinned(self, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, max_len, chunk=0):
+        """All tensor arguments are pinned CPU tensors (torch pin_memory=True)."""
+        r = lib().pmc_gzip_compress_batch_pinned(self.handle, _ptr(src), _ptr(src_off), _ptr(src_len),
+                                                 _n(src_len), _ptr(dst), _ptr(dst_off), _ptr(dst_cap),
+                                                 _ptr(dst_len), _ptr(rc), max_len, chunk)
+        if r != 0:
+            raise CodecUnavailable(f"pmc_gzip_compress_batch_pinned = {r}: {last_error()}")
+
+    def decompress_pinned(self, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, max_len, chunk=0):
+        r = lib().pmc_gzip_decompress_batch_pinned(self.handle, _ptr(src), _ptr(src_off), _ptr(src_len),
+                                                   _n(src_len), _ptr(dst), _ptr(dst_off), _ptr(dst_cap),
+                                                   _ptr(dst_len), _ptr(rc), max_len, chunk)
+        if r != 0:
+            raise CodecUnavailable(f"pmc_gzip_decompress_batch_pinned = {r}: {last_error()}")
 
 
 def _ptr(t):

@@ -326,3 +326,62 @@ def test_crc32_batch_vs_oracle(ctx, D):
     raw = buf.tobytes()
     bad = [i for i in range(len(lens)) if got[i] != O.crc32(raw[offs[i]:offs[i] + lens[i]])]
     assert not bad, [(int(lens[i]), int(offs[i]) % 4) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("chunk,packed", [(0, False), (1, False), (7, False), (64, False), (0, True), (1, True),
+                                          (7, True), (64, True)])
+def test_pinned_pipelined_batch_vs_oracle(ctx, golden, chunk, packed):
+    """pmc_gzip_{compress,decompress}_batch_pinned: ragged golden values (1 B .. 82 KB, LDS and HBM
+    kernel variants in one batch) in pinned host buffers with gaps between values, cut into chunks
+    whose copies overlap the neighbouring chunks' kernels; bit-exact vs the goldens and an exact
+    round trip.  Slot mode: outputs at dst_off, bytes past every chunk's slot range untouched.
+    Packed mode (dst_off NULL): outputs back to back in index order, failed values taking no bytes."""
+    import torch
+    pairs = [(r, g) for r, g in golden.pairs() if r][:300]
+    if packed:
+        pairs.insert(5, (b"\x00" * 40, None))  # placeholder slot made to fail below (cap too small)
+    n = len(pairs)
+    lens = np.array([len(r) for r, _ in pairs], dtype=np.int64)
+    gaps = np.random.default_rng(chunk).integers(0, 5, n)
+    soff = np.cumsum(np.concatenate([[3], (lens + gaps)[:-1]]))
+    src = torch.zeros(int(soff[-1] + lens[-1] + 64), dtype=torch.uint8).pin_memory()
+    for k, (r, _) in enumerate(pairs):
+        src[int(soff[k]):int(soff[k]) + len(r)] = torch.frombuffer(bytearray(r), dtype=torch.uint8)
+    caps = np.array([len(g) + 40 if g is not None else 8 for _, g in pairs], dtype=np.int64)
+    doff = np.concatenate([[0], np.cumsum(caps)[:-1]])
+    dst = torch.full((int(caps.sum()) + 64,), 0xEE, dtype=torch.uint8).pin_memory()
+    pin = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).pin_memory()  # noqa: E731
+    t_soff, t_slen = pin(soff, np.int64), pin(lens, np.int32)
+    t_doff, t_dcap = pin(doff, np.int64), pin(caps, np.int32)
+    dlen = torch.zeros(n, dtype=torch.int32).pin_memory()
+    rc = torch.full((n,), 7, dtype=torch.int32).pin_memory()
+    ctx.compress_pinned(src, t_soff, t_slen, dst, None if packed else t_doff, t_dcap, dlen, rc, int(lens.max()),
+                        chunk)
+    ok = np.array([g is not None for _, g in pairs])
+    rcn = rc.numpy()
+    assert (rcn[ok] == 0).all() and (rcn[~ok] != 0).all()
+    got_len = dlen.numpy().astype(np.int64) * ok
+    if packed:  # members back to back in index order
+        doff = np.concatenate([[0], np.cumsum(got_len)[:-1]])
+    raw = dst.numpy().tobytes()
+    bad = [k for k, (_, g) in enumerate(pairs) if g is not None and raw[doff[k]:doff[k] + int(dlen[k])] != g]
+    assert not bad, bad[:10]
+    end = int(got_len.sum()) if packed else len(raw) - 64
+    assert raw[end:] == b"\xee" * (len(raw) - end)
+    # decompress the good members where they lie into a fresh ragged buffer
+    keep = np.nonzero(ok)[0]
+    m_off, m_len = pin(doff[keep], np.int64), pin(got_len[keep], np.int32)
+    vlens = lens[keep]
+    boff = np.concatenate([[5], 5 + np.cumsum(vlens + 3)[:-1]])
+    back = torch.zeros(int(boff[-1] + vlens[-1] + 64), dtype=torch.uint8).pin_memory()
+    blen = torch.zeros(len(keep), dtype=torch.int32).pin_memory()
+    brc = torch.full((len(keep),), 7, dtype=torch.int32).pin_memory()
+    ctx.decompress_pinned(dst, m_off, m_len, back, None if packed else pin(boff, np.int64), pin(vlens, np.int32),
+                          blen, brc, int(lens.max()), chunk)
+    assert int((brc != 0).sum()) == 0
+    if packed:
+        boff = np.concatenate([[0], np.cumsum(vlens)[:-1]])
+    braw = back.numpy().tobytes()
+    bad = [j for j, k in enumerate(keep)
+           if int(blen[j]) != len(pairs[k][0]) or braw[boff[j]:boff[j] + vlens[j]] != pairs[k][0]]
+    assert not bad, bad[:10]
