@@ -105,14 +105,19 @@ int pmc_gzip_decompress_batch_host(pmc_ctx *ctx, const uint8_t *src, const uint6
 
 /* ---- batched, PINNED host memory, pipelined (the PCIe-inclusive path) --------------------
  * Same layout as the host-resident calls, but every pointer is host memory that the caller has
- * pinned (hipHostMalloc / hipHostRegister) and dst_off is required.  The batch is cut into
- * chunks of `chunk` values (0 = max(65536, n/16)); the H2D copy of chunk c+1 and the D2H copy
- * of chunk c-1 run on two context-owned copy streams beside chunk c's kernels, so the PCIe
- * legs hide behind the codec.  Chunk c's source bytes are copied as the range [min src_off,
- * max src_off+src_len) of its values and its destination range [min dst_off, max
- * dst_off+dst_cap) is written back whole.  max_len as for the device calls.  Returns after the
- * last chunk has landed in dst / dst_len / rc.  Replaces nothing in the reference (which has no
- * batch API); it is the host side of SURVEY.md §8(d)'s host-to-host rate. */
+ * pinned (hipHostMalloc / hipHostRegister).  The batch is cut into chunks of `chunk` values
+ * (0 = max(65536, n/16)); the H2D copy of chunk c+1 and the D2H copy of chunk c-1 run on two
+ * context-owned copy streams beside chunk c's kernels, so the PCIe legs hide behind the codec.
+ * Chunk c's source bytes are copied as the range [min src_off, max src_off+src_len) of its
+ * values.  max_len as for the device calls.  Returns after the last chunk has landed.
+ *   Slot mode (dst_off given): output i at dst + dst_off[i]; each chunk's destination range
+ *     [min dst_off, max dst_off+dst_cap) is written back whole.
+ *   Packed mode (dst_off NULL): outputs back to back in index order (output i at the sum of
+ *     dst_len[j] over j < i with rc[j] == 0; a failed value takes no bytes).  The device
+ *     compacts each chunk, so only the real output bytes cross PCIe; dst must hold
+ *     sum(dst_cap).  This is what a SET batch wants: ~C bytes per value back, not dst_cap.
+ * Replaces nothing in the reference (which has no batch API); it is the host side of
+ * SURVEY.md §8(d)'s host-to-host rate and the call a batched server path (§8 f1) makes. */
 int pmc_gzip_compress_batch_pinned(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
                                    const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
                                    const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
