@@ -70,6 +70,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--h2h", action="store_true", help="also time pinned H2D+kernel+D2H (host-to-host)")
     ap.add_argument("--h2h-chunk", type=int, default=0, help="values per chunk of the pipelined h2h leg (0 = n/16)")
+    ap.add_argument("--mix", action="store_true",
+                    help="BASELINE configs[2]: SET/GET mix over a device-resident compressed store instead")
+    ap.add_argument("--mix-keys", type=int, default=1_000_000)
+    ap.add_argument("--mix-ops", type=int, default=1_048_576)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (from scripts/pmc_traffic.py), if present")
     return ap.parse_args()
@@ -122,8 +126,124 @@ def cpu_baseline(corpus, args, index0):
             "cpu": cpu, "zlib": zv}
 
 
+def mix_bench(args):
+    """BASELINE.json configs[2] / SURVEY.md §8d cfg 3: 1M x 4 KiB JSON-slice values, batches of 65,536
+    ops, 50 % SET (compress a fresh value into the key's slot of a device-resident compressed store)
+    and 50 % GET (decompress a previously stored value), seed 7.
+
+    The store is one HBM slab of fixed slots (pmc_gzip_bound(vlen) bytes per key) plus a length per
+    key -- SURVEY §8f2's device-resident store.  Per batch, a random permutation of the key space
+    gives 32,768 SET keys and 32,768 disjoint GET keys, so op order inside a batch cannot change any
+    GET's answer.  The store is prefilled (untimed) with value index k for key k; SET j of batch b
+    stores fresh value index K + b*32768 + j.  Every GET is verified afterwards against the value
+    its key held (device-side compare against regenerated values)."""
+    import torch
+
+    import pmc_codec
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    L = pmc_codec.lib()
+    ctx = pmc_codec.Context(0)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    corpus_b = load_corpus()
+    corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).to(dev)
+    K, vlen, seed, bsz = args.mix_keys, args.vlen, 0x5EED, 65536
+    half = bsz // 2
+    nb = args.mix_ops // bsz
+    cap = pmc_codec.gzip_bound(vlen)
+    stride = (cap + 15) // 16 * 16
+
+    def gen(index, n, dst):
+        assert L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), seed, 0, 0, index.data_ptr(), n, vlen,
+                                dst.data_ptr(), sh) == 0
+
+    # ---- prefill the store: key k holds value index k ----------------------------------------
+    store = torch.empty(K * stride + 16, dtype=torch.uint8, device=dev)
+    slen = torch.zeros(K, dtype=torch.int32, device=dev)
+    ver = torch.arange(K, dtype=torch.int64, device=dev)
+    src = torch.empty(K * vlen + 16, dtype=torch.uint8, device=dev)
+    gen(ver, K, src)
+    koff = torch.arange(K, dtype=torch.int64, device=dev) * stride
+    rc = torch.zeros(K, dtype=torch.int32, device=dev)
+    ctx.compress_device(src, koff // stride * vlen, torch.full((K,), vlen, dtype=torch.int32, device=dev), store,
+                        koff, torch.full((K,), cap, dtype=torch.int32, device=dev), slen, rc, vlen, sh)
+    torch.cuda.synchronize()
+    assert int((rc != 0).sum()) == 0
+    del src
+
+    # ---- per-batch inputs (untimed): keys, fresh SET values ---------------------------------
+    g = torch.Generator(device="cpu").manual_seed(7)
+    perms = [torch.randperm(K, generator=g)[:bsz].to(dev) for _ in range(nb)]
+    set_keys = [p[:half].contiguous() for p in perms]
+    get_keys = [p[half:].contiguous() for p in perms]
+    set_idx = [K + b * half + torch.arange(half, dtype=torch.int64, device=dev) for b in range(nb)]
+    set_vals = torch.empty(nb * half * vlen + 16, dtype=torch.uint8, device=dev)
+    for b in range(nb):
+        gen(set_idx[b], half, set_vals[b * half * vlen:])
+    v_off = torch.arange(half, dtype=torch.int64, device=dev) * vlen
+    v_len = torch.full((half,), vlen, dtype=torch.int32, device=dev)
+    v_cap = torch.full((half,), cap, dtype=torch.int32, device=dev)
+    t_len = torch.zeros(half, dtype=torch.int32, device=dev)
+    s_rc = torch.zeros(nb, half, dtype=torch.int32, device=dev)
+    outs = torch.empty(nb * half * vlen + 16, dtype=torch.uint8, device=dev)
+    o_len = torch.zeros(nb, half, dtype=torch.int32, device=dev)
+    g_rc = torch.zeros(nb, half, dtype=torch.int32, device=dev)
+    g_ver = torch.zeros(nb, half, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+
+    def batch(b):
+        sk, gk = set_keys[b], get_keys[b]
+        # SET: compress the fresh values straight into their keys' store slots
+        ctx.compress_device(set_vals[b * half * vlen:], v_off, v_len, store, sk * stride, v_cap, t_len, s_rc[b],
+                            vlen, sh)
+        slen[sk] = t_len
+        ver[sk] = set_idx[b]
+        # GET: decompress the stored members of the GET keys
+        g_ver[b] = ver[gk]
+        ctx.decompress_device(store, gk * stride, slen[gk], outs[b * half * vlen:], v_off, v_len, o_len[b], g_rc[b],
+                              vlen, sh)
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for b in range(nb):
+        batch(b)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 1e3
+
+    # ---- verify every GET against the value its key held --------------------------------------
+    bad = int((s_rc != 0).sum()) + int((g_rc != 0).sum()) + int((o_len != vlen).sum())
+    want = torch.empty(half * vlen + 16, dtype=torch.uint8, device=dev)
+    mism = torch.zeros(1, dtype=torch.int32, device=dev)
+    for b in range(nb):
+        gen(g_ver[b].contiguous(), half, want)
+        assert L.pmc_compare_values(want.data_ptr(), v_off.data_ptr(), outs[b * half * vlen:].data_ptr(),
+                                    v_off.data_ptr(), v_len.data_ptr(), o_len[b].data_ptr(), half,
+                                    mism.data_ptr(), sh) == 0
+    torch.cuda.synchronize()
+    bad += int(mism.item())
+    ops = nb * bsz
+    gib = ops * vlen / 2 ** 30
+    print(json.dumps({
+        "metric": "SET/GET mix throughput over a device-resident compressed store (BASELINE configs[2])",
+        "value": gib / t, "unit": "GiB/s", "ops_per_s": ops / t, "n_gpus": 1, "ops": ops, "batches": nb,
+        "ms_per_batch": t / nb * 1e3, "higher_is_better": True, "dtype": "u8",
+        "data": f"synthetic: JSON slices of the reference's tests/data corpus (seed {seed:#x}), keys seed 7",
+        "config": {"workload": f"{K} keys x {vlen} B values, batches of {bsz} ops: 50% SET (compress into the "
+                               "key's HBM slot) / 50% GET (decompress a stored value), disjoint keys per batch",
+                   "keys": K, "value_bytes": vlen, "batch_ops": bsz},
+        "mismatches": bad}), flush=True)
+    ctx.close()
+
+
 def main():
     args = parse()
+    if args.mix:
+        if args.vlen == 1024:
+            args.vlen = 4096
+        return mix_bench(args)
     import numpy as np
     import torch
     import torch.distributed as dist
