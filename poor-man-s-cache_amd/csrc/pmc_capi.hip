@@ -249,9 +249,19 @@ Launch plan_lds(pmc_ctx *ctx, const void *kernel, uint64_t wave_bytes, uint64_t 
     Launch L;
     L.wave_bytes = wave_bytes;
     uint64_t fit = (kLdsPerCu - kCrcTabBytes) / wave_bytes;
+    // waves per block: the most resident waves per CU, then the widest block.  At 4 KiB values the
+    // front needs 25 KB per wave: 4-wave blocks (102 KB) fit once per CU (4 waves), 2-wave blocks
+    // three times (6 waves).
     L.wpb = (int)std::max<uint64_t>(1, std::min<uint64_t>(4, fit));
+    int per_cu = occupancy_blocks(kernel, 64 * L.wpb, kCrcTabBytes + L.wpb * wave_bytes);
+    for (int w = L.wpb - 1; w >= 1; w--) {
+        const int pc = occupancy_blocks(kernel, 64 * w, kCrcTabBytes + w * wave_bytes);
+        if (w * pc > L.wpb * per_cu) {
+            L.wpb = w;
+            per_cu = pc;
+        }
+    }
     L.lds = kCrcTabBytes + L.wpb * wave_bytes;
-    int per_cu = occupancy_blocks(kernel, 64 * L.wpb, L.lds);
     uint64_t need_blocks = (n_items + L.wpb - 1) / L.wpb;
     L.blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * per_cu, need_blocks));
     return L;
