@@ -59,3 +59,12 @@ def test_no_gpu_fails_loudly_or_works():
     h = ctypes.c_void_p()
     rc = pmc_codec.lib().pmc_ctx_create(0, ctypes.byref(h))
     assert rc == pmc_codec.E_NO_DEVICE
+
+
+def test_pinned_batch_rejects_bad_arguments_without_touching_a_device():
+    """pmc_gzip_*_batch_pinned validate before any HIP call: NULL context or arrays -> PMC_E_ARG."""
+    L = pmc_codec.lib()
+    buf = ctypes.create_string_buffer(64)
+    for fn in (L.pmc_gzip_compress_batch_pinned, L.pmc_gzip_decompress_batch_pinned):
+        assert fn(None, buf, buf, buf, 1, buf, None, buf, buf, buf, 16, 0) == pmc_codec.E_ARG
+        assert fn(None, None, None, None, 0, None, None, None, None, None, 0, 0) == pmc_codec.E_ARG
