@@ -270,6 +270,25 @@ def test_cpp_dropin_links_and_passes(ctx, golden):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_batch_codec_set_get(ctx, golden):
+    """pmc_batch::CompressForSet / DecompressForGet (dropin/batch_codec.*, the codec call of a batched
+    server path) make kvs.cpp's per-value decisions and return the reference's bytes."""
+    import pmc_codec
+    d = tempfile.mkdtemp(prefix="pmc_batch_")
+    for k, (name, data) in enumerate(golden.data_files):
+        r, g = golden.pair(k)
+        with open(os.path.join(d, name + ".gz"), "wb") as f:
+            f.write(g)
+    exe = os.path.join(d, "batch_codec_test")
+    pkg = os.path.dirname(pmc_codec.LIB_PATH)
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "poor-man-s-cache_amd", "dropin"),
+                           "-o", exe, os.path.join(ROOT, "tests", "host", "batch_codec_test.cpp"),
+                           "-L", pkg, "-lgzip_dropin", "-lpmc_codec", "-Wl,-rpath," + pkg])
+    r = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "data"), d], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_route_keys_vs_oracle(ctx, D):
     import ctypes
     import torch
