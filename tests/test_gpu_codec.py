@@ -404,3 +404,50 @@ def test_pinned_pipelined_batch_vs_oracle(ctx, golden, chunk, packed):
     bad = [j for j, k in enumerate(keep)
            if int(blen[j]) != len(pairs[k][0]) or braw[boff[j]:boff[j] + vlens[j]] != pairs[k][0]]
     assert not bad, bad[:10]
+
+
+def test_scattered_slots_in_place_store(ctx, D, golden):
+    """A device-resident store's access pattern (bench.py --mix): values read from and members written
+    to permuted, unaligned, non-monotonic slots of one slab, then decompressed from those slots into
+    another permuted layout; bit-exact against the reference's bytes and an exact round trip."""
+    import torch
+    import pmc_codec
+    pairs = [(r, g) for r, g in golden.pairs() if r][:400]
+    n = len(pairs)
+    rng = np.random.default_rng(0x5107)
+    lens = np.array([len(r) for r, _ in pairs], dtype=np.int64)
+    caps = np.array([pmc_codec.gzip_bound(int(x)) for x in lens], dtype=np.int64)
+    cstride, vstride = int(caps.max()) + 3, int(lens.max()) + 5
+
+    def layout(stride):
+        off = rng.permutation(n).astype(np.int64) * stride + rng.integers(0, 3, n)
+        return off, torch.from_numpy(off).cuda()
+
+    soff_h, soff = layout(vstride)
+    src = np.zeros(n * vstride + 64, dtype=np.uint8)
+    for k, (r, _) in enumerate(pairs):
+        src[soff_h[k]:soff_h[k] + len(r)] = np.frombuffer(r, dtype=np.uint8)
+    dsrc = torch.from_numpy(src).cuda()
+    coff_h, coff = layout(cstride)
+    store = torch.full((n * cstride + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+    slen = torch.from_numpy(lens.astype(np.int32)).cuda()
+    ccap = torch.from_numpy(caps.astype(np.int32)).cuda()
+    clen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    crc = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    ctx.compress_device(dsrc, soff, slen, store, coff, ccap, clen, crc, int(lens.max()), D.stream_handle())
+    sync()
+    assert int((crc != 0).sum()) == 0
+    st = store.cpu().numpy()
+    cl = clen.cpu().numpy()
+    bad = [k for k, (_, g) in enumerate(pairs) if st[coff_h[k]:coff_h[k] + cl[k]].tobytes() != g]
+    assert not bad, bad[:10]
+    boff_h, boff = layout(vstride)
+    back = torch.zeros(n * vstride + 64, dtype=torch.uint8, device="cuda")
+    blen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    brc = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    ctx.decompress_device(store, coff, clen, back, boff, slen, blen, brc, int(lens.max()), D.stream_handle())
+    sync()
+    assert int((brc != 0).sum()) == 0
+    bk = back.cpu().numpy()
+    bad = [k for k, (r, _) in enumerate(pairs) if bk[boff_h[k]:boff_h[k] + len(r)].tobytes() != r]
+    assert not bad, bad[:10]
