@@ -73,6 +73,7 @@ def parse():
     ap.add_argument("--mix", action="store_true",
                     help="BASELINE configs[2]: SET/GET mix over a device-resident compressed store instead")
     ap.add_argument("--mix-keys", type=int, default=1_000_000)
+    ap.add_argument("--mix-serial", action="store_true", help="SETs and GETs of a batch on one stream")
     ap.add_argument("--mix-ops", type=int, default=1_048_576)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (from scripts/pmc_traffic.py), if present")
@@ -193,22 +194,45 @@ def mix_bench(args):
     g_ver = torch.zeros(nb, half, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
 
+    # SETs of batch b run on stream A and its GETs on stream B: their keys are disjoint, so they may
+    # overlap (the GETs fill the CUs the front kernel's tail leaves idle).  B_b waits for A_(b-1)
+    # (a GET sees every earlier batch's SETs); A_(b+1) waits for B_b (no SET overwrites a slot a
+    # GET of an earlier batch still reads).  --mix-serial runs both on one stream.
+    sA = stream
+    sB = torch.cuda.Stream() if not args.mix_serial else stream
+    evA = [torch.cuda.Event() for _ in range(nb)]
+    evB = [torch.cuda.Event() for _ in range(nb)]
+
     def batch(b):
         sk, gk = set_keys[b], get_keys[b]
-        # SET: compress the fresh values straight into their keys' store slots
-        ctx.compress_device(set_vals[b * half * vlen:], v_off, v_len, store, sk * stride, v_cap, t_len, s_rc[b],
-                            vlen, sh)
-        slen[sk] = t_len
-        ver[sk] = set_idx[b]
-        # GET: decompress the stored members of the GET keys
-        g_ver[b] = ver[gk]
-        ctx.decompress_device(store, gk * stride, slen[gk], outs[b * half * vlen:], v_off, v_len, o_len[b], g_rc[b],
-                              vlen, sh)
+        if b > 0:
+            sA.wait_event(evB[b - 1])
+        with torch.cuda.stream(sA):
+            # SET: compress the fresh values straight into their keys' store slots
+            ctx.compress_device(set_vals[b * half * vlen:], v_off, v_len, store, sk * stride, v_cap, t_len, s_rc[b],
+                                vlen, sA.cuda_stream)
+            slen[sk] = t_len
+            ver[sk] = set_idx[b]
+            evA[b].record(sA)
+        if b > 0:
+            sB.wait_event(evA[b - 1])
+        with torch.cuda.stream(sB):
+            # GET: decompress the stored members of the GET keys
+            g_ver[b] = ver[gk]
+            ctx.decompress_device(store, gk * stride, slen[gk], outs[b * half * vlen:], v_off, v_len, o_len[b],
+                                  g_rc[b], vlen, sB.cuda_stream)
+            evB[b].record(sB)
 
+    # warm-up GET (untimed): sizes the decompress scratch; its outputs are overwritten by batch 0
+    ctx.decompress_device(store, get_keys[0] * stride, slen[get_keys[0]], outs, v_off, v_len, o_len[0], g_rc[0],
+                          vlen, sh)
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
+    sB.wait_event(e0)
     for b in range(nb):
         batch(b)
+    sA.wait_event(evB[nb - 1])
     e1.record(stream)
     torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / 1e3
@@ -233,7 +257,8 @@ def mix_bench(args):
         "data": f"synthetic: JSON slices of the reference's tests/data corpus (seed {seed:#x}), keys seed 7",
         "config": {"workload": f"{K} keys x {vlen} B values, batches of {bsz} ops: 50% SET (compress into the "
                                "key's HBM slot) / 50% GET (decompress a stored value), disjoint keys per batch",
-                   "keys": K, "value_bytes": vlen, "batch_ops": bsz},
+                   "keys": K, "value_bytes": vlen, "batch_ops": bsz,
+                   "streams": 1 if args.mix_serial else 2},
         "mismatches": bad}), flush=True)
     ctx.close()
 
