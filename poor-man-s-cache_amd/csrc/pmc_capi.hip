@@ -835,9 +835,9 @@ int pipe_init(pmc_ctx *ctx) {
 // dst_cap, compacts the results by a scan of dst_len (rc != 0 -> 0 bytes) and copies back only
 // those bytes, appended to dst; the host waits for chunk c's total (on the compute stream, after
 // its kernels) only once chunk c + 1's kernels are enqueued, so the device never idles on it.
-int pinned_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
-                 uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
-                 int32_t *rc, uint32_t max_len, uint32_t chunk) {
+int pinned_batch_run(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                     uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+                     int32_t *rc, uint32_t max_len, uint32_t chunk) {
     if (!ctx || !src || !src_off || !src_len || !dst || !dst_cap || !dst_len || !rc) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
     HIP_TRY(hipSetDevice(ctx->device));
@@ -939,6 +939,22 @@ int pinned_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_
     HIP_TRY(hipStreamSynchronize(P.d2h));
     P.busy[0] = P.busy[1] = false;
     return PMC_OK;
+}
+
+// On an error part of the batch may still be in flight on the three streams, reading and writing the
+// caller's buffers: drain them before returning, so the caller may free those buffers at once.
+int pinned_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                 uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+                 int32_t *rc, uint32_t max_len, uint32_t chunk) {
+    const int r = pinned_batch_run(ctx, dir, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len,
+                                   chunk);
+    if (r && ctx && ctx->pipe.h2d) {
+        (void)hipStreamSynchronize(ctx->pipe.h2d);
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamSynchronize(ctx->pipe.d2h);
+        ctx->pipe.busy[0] = ctx->pipe.busy[1] = false;
+    }
+    return r;
 }
 
 } // namespace
