@@ -97,11 +97,20 @@ def cpu_baseline(corpus, args, index0):
     seed = 0x5EED if args.kind == 0 else 0xA1B2
     n = args.cpu_sample
     vals = O.gen_values(corpus, seed, args.kind, index0, n, args.vlen)
+    single = None
     if O.ref_available():
         r = O.ref_bench(vals, cores)
         assert r["bad"] == 0
         t = r["t_compress"] + r["t_decompress"]
         kind, zv = "reference", O.ref().ref_zlib_version().decode()
+        # one core, the server's single request-handler thread (server.cpp:631-643)
+        n1 = min(n, 30_000)
+        r1 = O.ref_bench(vals[:n1], 1)
+        assert r1["bad"] == 0
+        g1 = n1 * args.vlen / 2 ** 30
+        single = {"value": g1 / (r1["t_compress"] + r1["t_decompress"]), "cores": 1,
+                  "compress_gib_s": g1 / r1["t_compress"], "decompress_gib_s": g1 / r1["t_decompress"],
+                  "sample": f"{n1} x {args.vlen} B values (indices {index0}..{index0 + n1 - 1})"}
     else:
         import time as _t
         n = min(n, 20_000)
@@ -124,7 +133,7 @@ def cpu_baseline(corpus, args, index0):
             "sample": f"{n} x {args.vlen} B values of the same workload (indices {index0}..{index0 + n - 1}), "
                       f"one GzipCompressor::Compress then Decompress per value, {cores} std::threads",
             "compress_gib_s": gib / r["t_compress"], "decompress_gib_s": gib / r["t_decompress"],
-            "cpu": cpu, "zlib": zv}
+            "cpu": cpu, "zlib": zv, "single_core": single}
 
 
 def mix_bench(args):
