@@ -245,23 +245,25 @@ uint64_t deflate_small_limit() {
     return lo;
 }
 
-Launch plan_lds(pmc_ctx *ctx, const void *kernel, uint64_t wave_bytes, uint64_t n_items) {
+// `extra` = dynamic LDS per block besides the waves' working sets (the CRC table; 0 for the front).
+Launch plan_lds(pmc_ctx *ctx, const void *kernel, uint64_t wave_bytes, uint64_t n_items,
+                uint64_t extra = kCrcTabBytes) {
     Launch L;
     L.wave_bytes = wave_bytes;
-    uint64_t fit = (kLdsPerCu - kCrcTabBytes) / wave_bytes;
+    uint64_t fit = (kLdsPerCu - extra) / wave_bytes;
     // waves per block: the most resident waves per CU, then the widest block.  At 4 KiB values the
     // front needs 25 KB per wave: 4-wave blocks (102 KB) fit once per CU (4 waves), 2-wave blocks
     // three times (6 waves).
     L.wpb = (int)std::max<uint64_t>(1, std::min<uint64_t>(4, fit));
-    int per_cu = occupancy_blocks(kernel, 64 * L.wpb, kCrcTabBytes + L.wpb * wave_bytes);
+    int per_cu = occupancy_blocks(kernel, 64 * L.wpb, extra + L.wpb * wave_bytes);
     for (int w = L.wpb - 1; w >= 1; w--) {
-        const int pc = occupancy_blocks(kernel, 64 * w, kCrcTabBytes + w * wave_bytes);
+        const int pc = occupancy_blocks(kernel, 64 * w, extra + w * wave_bytes);
         if (w * pc > L.wpb * per_cu) {
             L.wpb = w;
             per_cu = pc;
         }
     }
-    L.lds = kCrcTabBytes + L.wpb * wave_bytes;
+    L.lds = extra + L.wpb * wave_bytes;
     uint64_t need_blocks = (n_items + L.wpb - 1) / L.wpb;
     L.blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * per_cu, need_blocks));
     return L;
@@ -398,7 +400,11 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
     static const bool mono = getenv("PMC_DEFLATE_MONO") && atoi(getenv("PMC_DEFLATE_MONO"));
     if (!force_v1 && !mono) {
         const uint64_t fwb = deflate_front_wave_bytes(cap), bwb = deflate_back_wave_bytes(cap);
-        Launch Lf = plan_lds(ctx, (const void *)deflate_front_kernel, fwb, n);
+        // the front keeps no CRC table in LDS: its grid is sized for the blocks that really fit
+        // (PMC_FRONT_PLAN_CRC=1: the former plan, which reserved 1 KiB per block for it)
+        static const bool front_crc = getenv("PMC_FRONT_PLAN_CRC") && atoi(getenv("PMC_FRONT_PLAN_CRC"));
+        Launch Lf = plan_lds(ctx, (const void *)deflate_front_kernel, fwb, n, front_crc ? kCrcTabBytes : 0);
+        const size_t front_lds = Lf.lds - (front_crc ? kCrcTabBytes : 0);
         Launch Lb = plan_lds(ctx, (const void *)deflate_back_kernel, bwb, n);
         // chunk scratch budget (PMC_SPLIT_CHUNK_MB): 16 GiB of the 288 GiB holds 2.2M 1-KiB values, 5 launches
         // per 10M; measured best against 2-12 GiB (fewer kernel tails)
@@ -454,7 +460,7 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
             klaunch(ctx, PMC_K_DEFLATE_FRONT, st, [&] {
                 hipLaunchKernelGGL(deflate_front_kernel,
                                    dim3((unsigned)std::min<uint64_t>(Lf.blocks, (a.count + Lf.wpb - 1) / Lf.wpb)),
-                                   dim3(64 * Lf.wpb), Lf.lds - kCrcTabBytes, st, a);
+                                   dim3(64 * Lf.wpb), front_lds, st, a);
             });
             if (hipMemsetAsync(a.cD + a.count, 0, 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
             // trees visit order by used literal/length symbols (PMC_TREES_ORDER=0: index order)
