@@ -75,14 +75,49 @@ def parse():
     ap.add_argument("--mix-keys", type=int, default=1_000_000)
     ap.add_argument("--mix-serial", action="store_true", help="SETs and GETs of a batch on one stream")
     ap.add_argument("--mix-ops", type=int, default=1_048_576)
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (from scripts/pmc_traffic.py), if present")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
+                    help="PMC-derived HBM bytes and issue counters per launch (scripts/pmc_traffic.py); used "
+                         "only if its source_id matches the library's sources")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-core CPU baseline "
+                    "(0 = every core this process may run on)")
     return ap.parse_args()
 
 
 def load_corpus():
     d = os.path.join(ROOT, "tests", "golden", "data")
     return b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)) if f.endswith(".json"))
+
+
+def fullsize_bitexact(L, ctx, comp, coff, clen, n, vlen, kind, world, sh):
+    """Byte parity of ALL n members of the run against the reference (tests/golden/full_digests.json,
+    made by tests/golden/make_full_digests.py from the reference's own Compress): the device takes the
+    CRC-32 of every member (pmc_crc32_batch), the host hashes the (length, CRC) records with SHA-256.
+    Returns {"bitexact": bool, ...}, or None when no digest covers this workload (e.g. N > 1 ranks,
+    whose routed key subsets differ)."""
+    import hashlib
+    import numpy as np
+    import torch
+    if world != 1:
+        return None
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "full_digests.json")) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    want = None
+    for st in doc["sets"]:
+        if st["vlen"] == vlen and st["kind"] == kind and str(n) in st["prefixes"]:
+            want = st["prefixes"][str(n)]
+    if want is None:
+        return None
+    mcrc = torch.zeros(n, dtype=torch.int32, device=comp.device)
+    assert L.pmc_crc32_batch(ctx.handle, comp.data_ptr(), coff.data_ptr(), clen.data_ptr(), n, mcrc.data_ptr(),
+                             sh) == 0
+    rec = torch.stack([clen, mcrc], dim=1).cpu().numpy().astype("<u4")
+    got = hashlib.sha256(rec.tobytes()).hexdigest()
+    return {"bitexact": got == want["sha256"], "members": n, "sha256": got,
+            "reference": "tests/golden/full_digests.json (reference GzipCompressor::Compress, zlib "
+                         f"{doc.get('zlib_version')}): sha256 over (u32 len, u32 crc32) of every member"}
 
 
 def cpu_baseline(corpus, args, index0):
@@ -93,7 +128,17 @@ def cpu_baseline(corpus, args, index0):
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    cores = max(1, min(16, cores))  # the box's CPU share for one GPU
+    quota = None  # a cgroup CPU quota caps what the threads can get (cpu.max: "<quota> <period>")
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    # one thread per CPU this process may use: the affinity set, capped by the cgroup quota (the GPU
+    # box runs each GPU's job in a 16-CPU share of a 2 x 64-core host; more threads would only
+    # time-slice the same share)
+    cores = args.cpu_threads or max(1, min(cores, int(quota) if quota else cores))
     seed = 0x5EED if args.kind == 0 else 0xA1B2
     n = args.cpu_sample
     vals = O.gen_values(corpus, seed, args.kind, index0, n, args.vlen)
@@ -129,7 +174,28 @@ def cpu_baseline(corpus, args, index0):
             cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
     except OSError:
         pass
-    return {"value": gib / t, "unit": "GiB/s", "cores": cores, "kind": kind,
+    host_cores = None  # physical cores of the host (lscpu's Core(s) per socket x Socket(s))
+    try:
+        phys = set()
+        with open("/proc/cpuinfo") as f:
+            pid = core = None
+            for line in f:
+                if line.startswith("physical id"):
+                    pid = line.split(":")[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":")[1].strip()
+                    phys.add((pid, core))
+        host_cores = len(phys) or None
+    except OSError:
+        pass
+    all_core = None
+    if single and host_cores:
+        # linear upper bound: every physical core of the host running the reference at the one-core rate
+        all_core = {"value": single["value"] * host_cores, "cores": host_cores,
+                    "note": "estimate = single-core rate x physical cores (no shared-resource losses); the "
+                            "measured figure above is what the job's CPU share delivers"}
+    return {"value": gib / t, "unit": "GiB/s", "cores": cores, "kind": kind, "cgroup_cpu_quota": quota,
+            "host_physical_cores": host_cores, "all_host_cores_estimate": all_core,
             "sample": f"{n} x {args.vlen} B values of the same workload (indices {index0}..{index0 + n - 1}), "
                       f"one GzipCompressor::Compress then Decompress per value, {cores} std::threads",
             "compress_gib_s": gib / r["t_compress"], "decompress_gib_s": gib / r["t_decompress"],
@@ -370,6 +436,7 @@ def main():
     torch.cuda.synchronize()
     bad = int(mism.item()) + int((crc != 0).sum().item()) + int((brc != 0).sum().item())
     comp_bytes = int(clen.to(torch.int64).sum().item())
+    bitexact = fullsize_bitexact(L, ctx, comp, coff, clen, n, vlen, args.kind, world, sh)
 
     (t_step_s, tc_max, td_max), (total_bytes, total_comp, total_bad) = reduce_over_ranks(
         [wall / args.steps, tc, td], [float(n * vlen), float(comp_bytes), float(bad)], world, dev)
@@ -395,15 +462,21 @@ def main():
         dom = max(ckinds, key=lambda k: ktimes[k][0])
         dom_ms, dom_launches = ktimes[dom]
         avg_launch_s = dom_ms / dom_launches / 1e3
-        alg_launch = alg_c / dom_launches  # the launches split the batch into equal chunks
+        alg_launch = alg_c / dom_launches  # mean over the launches (chunks of the batch; the last one is shorter)
         achieved = alg_launch / avg_launch_s / 1e9
-        traffic = None  # measured HBM bytes per launch of that kernel (scripts/pmc_traffic.py)
+        # measured HBM bytes per launch of that kernel and its issue counters (scripts/pmc_traffic.py),
+        # quoted only when measured on these kernel sources and this workload
+        traffic, issue, tsrc = None, None, None
         if os.path.exists(args.traffic):
             try:
                 with open(args.traffic) as f:
                     tj = json.load(f)
-                if tj.get("n") == n and tj.get("vlen") == vlen and tj.get("kind") == args.kind:
-                    traffic = tj.get("kernels", {}).get(pmc_codec.KERNEL_NAMES[dom], {}).get("hbm_bytes_per_launch")
+                if (tj.get("n") == n and tj.get("vlen") == vlen and tj.get("kind") == args.kind
+                        and tj.get("source_id") == pmc_codec.source_id()):
+                    kj = tj.get("kernels", {}).get(pmc_codec.KERNEL_NAMES[dom], {})
+                    traffic = kj.get("hbm_bytes_per_launch")
+                    issue = kj.get("issue")
+                    tsrc = os.path.relpath(args.traffic, ROOT)
             except (OSError, ValueError):
                 traffic = None
         out = {
@@ -413,12 +486,14 @@ def main():
             "data": "synthetic: JSON slices of the reference's tests/data corpus (SURVEY.md §8d generator, "
                     f"seed {seed:#x})" if args.kind == 0 else "synthetic: random [A-Za-z0-9]",
             "config": {"workload": f"{n} x {vlen} B values per GPU ({'JSON-slice' if args.kind == 0 else 'alnum'}), "
-                                   "batched gzip level-9 compress + decompress, device-resident, zlib-bit-exact",
+                                   "batched gzip level-9 compress + decompress, device-resident, byte-checked "
+                                   "against the reference (fullsize_parity)",
                        "values_per_gpu": n, "value_bytes": vlen, "total_values": n * world,
                        "partition": "MurmurHash3_x64_128('key'+i)[0] % 128 % n_gpus (NUM_SHARDS=128)",
                        "parallelism": f"shard-partitioned x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                         "issue": issue,
                          "kernel": pmc_codec.KERNEL_NAMES[dom],
                          "alg_bytes_per_launch": alg_launch, "avg_launch_ms": avg_launch_s * 1e3,
                          "launches_per_step": dom_launches,
@@ -429,6 +504,7 @@ def main():
             "decompress_roofline_frac": alg_d / td / 1e9 / HBM_PEAK_GBS,
             "ratio": total_comp / total_bytes, "verified_values": int(total_bytes // vlen),
             "mismatches": int(total_bad),
+            "fullsize_parity": bitexact,
         }
         if h2h:
             out["host_to_host"] = h2h

@@ -34,7 +34,12 @@ extern "C" {
 #define PMC_E_CAPACITY (-101)    /* output capacity too small (batched API only)           */
 #define PMC_E_ARG (-102)         /* invalid argument                                       */
 
-typedef struct pmc_ctx pmc_ctx; /* one device + streams + scratch; not thread-safe */
+/* One device + streams + scratch.  The host-memory calls (single value, *_batch_host,
+ * *_batch_pinned) lock the context, so threads may share one (the drop-in shares the default
+ * context, keeping the reference's reentrant static methods reentrant) and they restore the
+ * caller's current HIP device.  The device-resident batch calls only enqueue work: see their
+ * note on streams below. */
+typedef struct pmc_ctx pmc_ctx;
 
 /* Create a context on HIP device `device` (gfx950).  Returns PMC_OK or PMC_E_NO_DEVICE. */
 int pmc_ctx_create(int device, pmc_ctx **out);
@@ -66,8 +71,13 @@ uint32_t pmc_gzip_isize(const void *in, size_t in_len);
  * rc[i].  All arrays are device pointers; the call only enqueues work on `stream`
  * (hipStream_t, NULL = legacy default stream) and returns.  max_len is an upper bound on
  * src_len[] (for compress) or on the decompressed sizes (for decompress); it selects the
- * kernel variant (LDS-resident vs HBM-resident working set).  Values are independent, so
- * any batch may be split arbitrarily (across calls, streams or GPUs).
+ * kernel variant (LDS-resident vs HBM-resident working set).  Compress: a value with
+ * src_len[i] > max_len is not compressed; it gets rc[i] = PMC_E_ARG, dst_len[i] = 0
+ * (checked on the device).  Values are independent, so a batch may be split arbitrarily
+ * across calls and GPUs.  Scratch is per context and per direction: the library orders two
+ * compress calls (or two decompress calls) of one context that are issued on different
+ * streams (the later one waits for the earlier one on the device); a compress and a
+ * decompress call of one context may run concurrently on two streams.
  * Compress: src_len[i] == 0 -> rc PMC_INVALID_INPUT (reference semantics).  Input bytes
  *   may contain NULs (binary safe; the single-value drop-in keeps the reference's strlen).
  * Decompress: dst_cap[i] must be >= the decompressed size (ISIZE); use
@@ -110,8 +120,12 @@ int pmc_gzip_decompress_batch_host(pmc_ctx *ctx, const uint8_t *src, const uint6
  * context-owned copy streams beside chunk c's kernels, so the PCIe legs hide behind the codec.
  * Chunk c's source bytes are copied as the range [min src_off, max src_off+src_len) of its
  * values.  max_len as for the device calls.  Returns after the last chunk has landed.
- *   Slot mode (dst_off given): output i at dst + dst_off[i]; each chunk's destination range
- *     [min dst_off, max dst_off+dst_cap) is written back whole.
+ *   Slot mode (dst_off given): output i at dst + dst_off[i].  If a chunk's slots tile one range
+ *     in index order (dst_off[i+1] == dst_off[i] + dst_cap[i]) that range is written back whole
+ *     (slot bytes past dst_len[i], and failed values' slots, hold unspecified bytes); any other
+ *     layout (gaps, permuted or interleaved slots) is compacted on the device and each output is
+ *     copied to its dst_off on the host, so only [dst_off[i], dst_off[i] + dst_len[i]) of
+ *     successful values is written.
  *   Packed mode (dst_off NULL): outputs back to back in index order (output i at the sum of
  *     dst_len[j] over j < i with rc[j] == 0; a failed value takes no bytes).  The device
  *     compacts each chunk, so only the real output bytes cross PCIe; dst must hold

@@ -122,6 +122,9 @@ def ref():
         R.ref_bench.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(ctypes.c_uint64)]
+        R.ref_member_records.restype = ctypes.c_int
+        R.ref_member_records.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_void_p]
         _REF = R
     return _REF
 
@@ -147,6 +150,32 @@ def ref_decompress(gz: bytes):
     if p.value:
         R.ref_free(p)
     return rc, data
+
+
+def member_records_digest(lens: np.ndarray, crcs: np.ndarray, h=None):
+    """Digest of a compressed set (tests/golden/full_digests.json): SHA-256 over the records
+    (u32 LE member length, u32 LE CRC-32 of the member bytes), value order.  Pass `h` to feed
+    a running hashlib object chunk by chunk."""
+    import hashlib
+    rec = np.empty((len(lens), 2), dtype="<u4")
+    rec[:, 0] = lens
+    rec[:, 1] = crcs
+    if h is None:
+        h = hashlib.sha256()
+    h.update(rec.tobytes())
+    return h
+
+
+def ref_member_records(values: np.ndarray, nthreads: int):
+    """(lens, crcs) of the reference Compress over every row of `values`."""
+    R = ref()
+    n, vlen = values.shape
+    lens = np.zeros(n, np.uint32)
+    crcs = np.zeros(n, np.uint32)
+    bad = R.ref_member_records(values.ctypes.data_as(ctypes.c_void_p), n, vlen, nthreads,
+                               lens.ctypes.data_as(ctypes.c_void_p), crcs.ctypes.data_as(ctypes.c_void_p))
+    assert bad == 0
+    return lens, crcs
 
 
 def ref_bench(values: np.ndarray, nthreads: int):

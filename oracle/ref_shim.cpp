@@ -69,4 +69,34 @@ int ref_bench(const uint8_t *values, uint32_t n, uint32_t vlen, int nthreads, do
     for (auto &c : comp) delete[] c.data;
     return bad.load();
 }
+
+// Full-size parity records (tests/golden/make_full_digests.py): value i of vlen bytes goes
+// through the reference Compress; lens[i] = member size, crcs[i] = CRC-32 (zlib crc32) of the
+// member's bytes.  The digest of a set is SHA-256 over the (u32 len, u32 crc) records, so a GPU
+// run can check all 10M members of the headline workload without moving them to the host.
+// Returns the number of values whose Compress failed.
+int ref_member_records(const uint8_t *values, uint32_t n, uint32_t vlen, int nthreads, uint32_t *lens,
+                       uint32_t *crcs) {
+    std::atomic<int> bad{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; t++)
+        th.emplace_back([&, t] {
+            std::vector<char> s(vlen + 1);
+            for (uint32_t i = t; i < n; i += nthreads) {
+                memcpy(s.data(), values + (uint64_t)i * vlen, vlen);
+                s[vlen] = 0;
+                CompressResult c = GzipCompressor::Compress(s.data());
+                if (c.operationResult != 0) {
+                    bad++;
+                    lens[i] = crcs[i] = 0;
+                    continue;
+                }
+                lens[i] = (uint32_t)c.size;
+                crcs[i] = (uint32_t)crc32(0L, (const Bytef *)c.data, (uInt)c.size);
+                delete[] c.data;
+            }
+        });
+    for (auto &x : th) x.join();
+    return bad.load();
+}
 }

@@ -169,12 +169,18 @@ struct pmc_ctx {
     DevBuf split;                // chunk arrays of the split small-value pipeline
     DevBuf crcx;                 // inflate: CRC-32 trailers from the lane kernel
     DevBuf order;                // inflate: lane visit order (bins | member indices)
+    // per direction (0 compress, 1 decompress): the event recorded after the last batch call and its
+    // stream; a call on another stream waits for it, since both use the direction's scratch
+    hipEvent_t dir_ev[2] = {};
+    hipStream_t dir_st[2] = {};
+    bool dir_used[2] = {false, false};
     bool prof = false;           // pmc_ctx_profile: bracket every launch with events
     struct KRec {
         int kind;
         hipEvent_t a, b;
     };
     std::vector<KRec> krecs;
+    std::mutex host_mu;          // host-API calls (host_batch, pinned_batch) of this context, one at a time
     DevBuf staging;              // device side of host-API calls
     uint64_t *dbg = nullptr;     // diagnostic stamp sums (PMC_STAMPS builds)
     HostBuf pinned;              // host side of host-API calls
@@ -184,7 +190,8 @@ struct pmc_ctx {
         hipStream_t h2d = nullptr, d2h = nullptr;
         hipEvent_t in[2] = {}, out[2] = {}, done[2] = {};
         DevBuf slot[2];
-        HostBuf total;           // packed mode: each slot's chunk total, read by the host
+        HostBuf total;           // compacted chunks: each slot's chunk total, read by the host
+        HostBuf bounce[2];       // slot mode, compacted chunk: outputs on their way to dst_off
         bool busy[2] = {false, false};
     } pipe;
 };
@@ -207,6 +214,20 @@ void klaunch(pmc_ctx *ctx, int kind, hipStream_t st, F launch) {
     launch();
     (void)hipEventRecord(r.b, st);
     ctx->krecs.push_back(r);
+}
+
+// Same-direction batch calls of one context share its scratch: a call issued on a different stream
+// than the previous one of its direction first waits (on the device) for that call to finish.
+int dir_enter(pmc_ctx *ctx, int dir, hipStream_t st) {
+    if (ctx->dir_used[dir] && ctx->dir_st[dir] != st)
+        if (hipStreamWaitEvent(st, ctx->dir_ev[dir], 0) != hipSuccess) return PMC_E_NO_DEVICE;
+    return PMC_OK;
+}
+int dir_leave(pmc_ctx *ctx, int dir, hipStream_t st) {
+    if (hipEventRecord(ctx->dir_ev[dir], st) != hipSuccess) return PMC_E_NO_DEVICE;
+    ctx->dir_st[dir] = st;
+    ctx->dir_used[dir] = true;
+    return PMC_OK;
 }
 
 struct Launch {
@@ -313,7 +334,9 @@ PMC_API int pmc_ctx_create(int device, pmc_ctx **out) {
     pmc_ctx *c = new pmc_ctx;
     c->device = device;
     c->cus = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->dir_ev[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->dir_ev[1], hipEventDisableTiming) != hipSuccess) {
         delete c;
         return PMC_E_NO_DEVICE;
     }
@@ -346,9 +369,13 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
             c->pipe.slot[k].release();
         }
         c->pipe.total.release();
+        c->pipe.bounce[0].release();
+        c->pipe.bounce[1].release();
         (void)hipStreamDestroy(c->pipe.h2d);
         (void)hipStreamDestroy(c->pipe.d2h);
     }
+    for (int k = 0; k < 2; k++)
+        if (c->dir_ev[k]) (void)hipEventDestroy(c->dir_ev[k]);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -368,13 +395,16 @@ PMC_API uint32_t pmc_gzip_isize(const void *in, size_t in_len) {
     return p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
-PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
-                                    const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
-                                    const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
-                                    void *stream) {
+static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                               uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap,
+                               uint32_t *dst_len, int32_t *rc, uint32_t max_len, void *stream) {
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
+    if (max_len == 0) max_len = 1;
     hipStream_t st = (hipStream_t)stream;
+    // src_len[i] > max_len: no variant below claims the value; it gets PMC_E_ARG on the device
+    hipLaunchKernelGGL(arg_check_kernel, dim3((unsigned)std::min<uint64_t>(((uint64_t)n + 255) / 256, 2048)),
+                       dim3(256), 0, st, src_len, (uint64_t)n, (uint64_t)max_len, rc, dst_len);
     DeflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, nullptr,
                   ctx->dbg, -1};
     if (const char *e = getenv("PMC_STOP_AFTER")) a.stop_after = atoi(e); // diagnostic builds only
@@ -543,10 +573,10 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
 
 static uint64_t inflate_lds_out_limit() { return 48 * 1024; }
 
-PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
-                                      const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
-                                      const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
-                                      void *stream) {
+static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                 const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
+                                 const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
+                                 void *stream) {
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
     hipStream_t st = (hipStream_t)stream;
@@ -622,6 +652,34 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
     return PMC_OK;
 }
 
+PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                    const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
+                                    const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
+                                    void *stream) {
+    if (!ctx) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    hipStream_t st = (hipStream_t)stream;
+    int r = dir_enter(ctx, 0, st);
+    if (r) return r;
+    r = compress_batch_body(ctx, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len, stream);
+    const int r2 = dir_leave(ctx, 0, st);
+    return r ? r : r2;
+}
+
+PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
+                                      const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
+                                      const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
+                                      void *stream) {
+    if (!ctx) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    hipStream_t st = (hipStream_t)stream;
+    int r = dir_enter(ctx, 1, st);
+    if (r) return r;
+    r = decompress_batch_body(ctx, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len, stream);
+    const int r2 = dir_leave(ctx, 1, st);
+    return r ? r : r2;
+}
+
 PMC_API int pmc_ctx_profile(pmc_ctx *ctx, int enable) {
     if (!ctx) return PMC_E_ARG;
     ctx->prof = enable != 0;
@@ -667,11 +725,26 @@ PMC_API int pmc_gzip_isize_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_
 namespace {
 enum Dir { kCompress, kDecompress };
 
+// A host-API call holds its context's lock (the staging buffers, pinned pipe and default context
+// are shared by every thread that calls the drop-in) and leaves the caller's current device as
+// it found it.
+struct HostCall {
+    std::lock_guard<std::mutex> lock;
+    int prev = -1;
+    explicit HostCall(pmc_ctx *ctx) : lock(ctx->host_mu) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~HostCall() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
                uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
                int32_t *rc) {
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
+    HostCall guard(ctx);
     HIP_TRY(hipSetDevice(ctx->device));
     // packed device layout: src bytes back to back, dst slots back to back
     uint64_t in_bytes = 0, out_bytes = 0, max_len = 0;
@@ -836,11 +909,16 @@ int pipe_init(pmc_ctx *ctx) {
 //   d2h:    dst_len, rc, then the chunk's destination bytes              -> event done[s]
 // and chunk c + 2 reuses slot s after done[s].  Chunk c's source bytes are the range
 // [min src_off, max src_off + src_len) of its values (packed layouts copy exactly their bytes).
-// Slot mode (dst_off given): the destination range [min dst_off, max dst_off + dst_cap) is copied
-// back whole.  Packed mode (dst_off null): the device lays the chunk's slots out by a scan of
-// dst_cap, compacts the results by a scan of dst_len (rc != 0 -> 0 bytes) and copies back only
-// those bytes, appended to dst; the host waits for chunk c's total (on the compute stream, after
-// its kernels) only once chunk c + 1's kernels are enqueued, so the device never idles on it.
+// Destinations, three ways:
+//   tiled slots (dst_off given, and the chunk's slots tile one range in index order:
+//     dst_off[i + 1] == dst_off[i] + dst_cap[i]): the range is copied back whole, straight into dst;
+//   any other slot layout (gaps, permuted or interleaved slots): the device compacts the chunk's
+//     outputs, they land in a pinned bounce buffer and the host copies each output to its dst_off,
+//     so no byte outside [dst_off[i], dst_off[i] + dst_len[i]) of a successful value is written;
+//   packed mode (dst_off null): the compacted bytes are appended to dst.
+// A compacted chunk's device slots are laid out by a scan of dst_cap, its results compacted by a
+// scan of dst_len (rc != 0 -> 0 bytes); the host waits for chunk c's byte total (on the compute
+// stream, after its kernels) only once chunk c + 1's kernels are enqueued, so the device never idles.
 int pinned_batch_run(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
                      uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
                      int32_t *rc, uint32_t max_len, uint32_t chunk) {
@@ -857,17 +935,46 @@ int pinned_batch_run(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *
     volatile uint64_t *h_total = (volatile uint64_t *)P.total.p;  // chunk totals, slot s at [s]
     uint8_t *d_pk[2] = {nullptr, nullptr};
     uint64_t out_pos = 0;
-    // packed mode: chunk c's bytes go back once its total is known (called after chunk c + 1 is enqueued)
+    // slot mode, compacted chunk: its outputs wait in bounce[s] until done[s], then go to dst_off
+    struct Pend {
+        bool on = false;
+        uint32_t a = 0, m = 0;
+    } pend[2];
+    auto scatter = [&](uint32_t s) -> int {
+        if (!pend[s].on) return PMC_OK;
+        HIP_TRY(hipEventSynchronize(P.done[s]));
+        const uint8_t *b = (const uint8_t *)P.bounce[s].p;
+        uint64_t p = 0;
+        for (uint32_t i = pend[s].a; i < pend[s].a + pend[s].m; i++)
+            if (rc[i] == 0) {
+                memcpy(dst + dst_off[i], b + p, dst_len[i]);
+                p += dst_len[i];
+            }
+        pend[s].on = false;
+        return PMC_OK;
+    };
+    // compacted chunk c's bytes go back once its total is known (called after chunk c + 1 is enqueued)
     auto finish = [&](uint32_t c) -> int {
         const uint32_t s = c & 1;
         HIP_TRY(hipEventSynchronize(P.out[s]));
         const uint64_t tot = h_total[s];
+        uint8_t *to = dst + out_pos;
+        if (!packed) {
+            int e = scatter(s);  // chunk c - 2's outputs leave bounce[s] first
+            if (e) return e;
+            if ((e = P.bounce[s].ensure(tot + 64))) return e;
+            to = (uint8_t *)P.bounce[s].p;
+            pend[s].on = true;
+            pend[s].a = c * chunk;
+            pend[s].m = std::min<uint32_t>(chunk, n - c * chunk);
+        }
         HIP_TRY(hipStreamWaitEvent(P.d2h, P.out[s], 0));
-        if (tot) HIP_TRY(hipMemcpyAsync(dst + out_pos, d_pk[s], tot, hipMemcpyDeviceToHost, P.d2h));
+        if (tot) HIP_TRY(hipMemcpyAsync(to, d_pk[s], tot, hipMemcpyDeviceToHost, P.d2h));
         HIP_TRY(hipEventRecord(P.done[s], P.d2h));
-        out_pos += tot;
+        if (packed) out_pos += tot;
         return PMC_OK;
     };
+    int64_t unfinished = -1;  // a compacted chunk whose D2H is not enqueued yet
     for (uint32_t c = 0; c < nchunks; c++) {
         const uint32_t a = c * chunk, m = std::min<uint32_t>(chunk, n - a), s = c & 1;
         uint64_t sb = ~0ull, se = 0, db = ~0ull, de = 0;
@@ -875,18 +982,20 @@ int pinned_batch_run(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *
             sb = std::min(sb, src_off[i]);
             se = std::max(se, src_off[i] + src_len[i]);
         }
-        if (packed) {
+        bool compact = packed;
+        if (!packed) {
+            for (uint32_t i = a; i + 1 < a + m && !compact; i++) compact = dst_off[i + 1] != dst_off[i] + dst_cap[i];
+            db = dst_off[a];
+            de = dst_off[a + m - 1] + dst_cap[a + m - 1];
+        }
+        if (compact) {
             db = 0;
+            de = 0;
             for (uint32_t i = a; i < a + m; i++) de += dst_cap[i];
-        } else {
-            for (uint32_t i = a; i < a + m; i++) {
-                db = std::min(db, dst_off[i]);
-                de = std::max(de, dst_off[i] + dst_cap[i]);
-            }
         }
         const uint32_t nb = (m + kScanBlock - 1) / kScanBlock;
         const uint64_t meta = al(m * 8ull) * 3 + al(m * 4ull) * 4 + al((nb + 1) * 8ull);
-        const uint64_t need = meta + al(se - sb + 16) + al(de - db + 16) * (packed ? 2 : 1);
+        const uint64_t need = meta + al(se - sb + 16) + al(de - db + 16) * (compact ? 2 : 1);
         if (need > P.slot[s].cap) {
             // the slot's previous chunk must have drained before it is reallocated
             if (P.busy[s]) HIP_TRY(hipEventSynchronize(P.done[s]));
@@ -904,23 +1013,23 @@ int pinned_batch_run(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *
         d_pk[s] = d_dst + al(de - db + 16);
         if (P.busy[s]) HIP_TRY(hipStreamWaitEvent(P.h2d, P.done[s], 0));
         HIP_TRY(hipMemcpyAsync(d_soff, src_off + a, m * 8ull, hipMemcpyHostToDevice, P.h2d));
-        if (!packed) HIP_TRY(hipMemcpyAsync(d_doff, dst_off + a, m * 8ull, hipMemcpyHostToDevice, P.h2d));
+        if (!compact) HIP_TRY(hipMemcpyAsync(d_doff, dst_off + a, m * 8ull, hipMemcpyHostToDevice, P.h2d));
         HIP_TRY(hipMemcpyAsync(d_slen, src_len + a, m * 4ull, hipMemcpyHostToDevice, P.h2d));
         HIP_TRY(hipMemcpyAsync(d_dcap, dst_cap + a, m * 4ull, hipMemcpyHostToDevice, P.h2d));
         HIP_TRY(hipMemcpyAsync(d_src, src + sb, se - sb, hipMemcpyHostToDevice, P.h2d));
         HIP_TRY(hipEventRecord(P.in[s], P.h2d));
         HIP_TRY(hipStreamWaitEvent(ctx->stream, P.in[s], 0));
         hipLaunchKernelGGL(rebase_kernel, dim3(std::min<uint32_t>((m + 255) / 256, 1024)), dim3(256), 0, ctx->stream,
-                           d_soff, packed ? nullptr : d_doff, m, sb, db);
+                           d_soff, compact ? nullptr : d_doff, m, sb, db);
         HIP_TRY(hipGetLastError());
-        if (packed && (r = scan_u32(d_dcap, nullptr, m, d_doff, d_bsum, ctx->stream))) return r;
+        if (compact && (r = scan_u32(d_dcap, nullptr, m, d_doff, d_bsum, ctx->stream))) return r;
         r = dir == kCompress
                 ? pmc_gzip_compress_batch(ctx, d_src, d_soff, d_slen, m, d_dst, d_doff, d_dcap, d_dlen, d_rc,
                                           max_len, ctx->stream)
                 : pmc_gzip_decompress_batch(ctx, d_src, d_soff, d_slen, m, d_dst, d_doff, d_dcap, d_dlen, d_rc,
                                             max_len, ctx->stream);
         if (r) return r;
-        if (packed) {
+        if (compact) {
             if ((r = scan_u32(d_dlen, d_rc, m, d_poff, d_bsum, ctx->stream))) return r;
             hipLaunchKernelGGL(compact_kernel, dim3(std::min<uint32_t>((m + 3) / 4, 8192)), dim3(256), 0,
                                ctx->stream, d_dst, d_doff, d_dlen, d_rc, d_poff, m, d_pk[s]);
@@ -929,19 +1038,24 @@ int pinned_batch_run(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *
             HIP_TRY(hipMemcpyAsync(rc + a, d_rc, m * 4ull, hipMemcpyDeviceToHost, ctx->stream));
             HIP_TRY(hipMemcpyAsync((void *)(h_total + s), d_bsum + nb, 8, hipMemcpyDeviceToHost, ctx->stream));
             HIP_TRY(hipEventRecord(P.out[s], ctx->stream));
-            P.busy[s] = true;
-            if (c > 0 && (r = finish(c - 1))) return r;
-            continue;
+        } else {
+            HIP_TRY(hipEventRecord(P.out[s], ctx->stream));
+            HIP_TRY(hipStreamWaitEvent(P.d2h, P.out[s], 0));
+            HIP_TRY(hipMemcpyAsync(dst_len + a, d_dlen, m * 4ull, hipMemcpyDeviceToHost, P.d2h));
+            HIP_TRY(hipMemcpyAsync(rc + a, d_rc, m * 4ull, hipMemcpyDeviceToHost, P.d2h));
+            HIP_TRY(hipMemcpyAsync(dst + db, d_dst, de - db, hipMemcpyDeviceToHost, P.d2h));
+            HIP_TRY(hipEventRecord(P.done[s], P.d2h));
         }
-        HIP_TRY(hipEventRecord(P.out[s], ctx->stream));
-        HIP_TRY(hipStreamWaitEvent(P.d2h, P.out[s], 0));
-        HIP_TRY(hipMemcpyAsync(dst_len + a, d_dlen, m * 4ull, hipMemcpyDeviceToHost, P.d2h));
-        HIP_TRY(hipMemcpyAsync(rc + a, d_rc, m * 4ull, hipMemcpyDeviceToHost, P.d2h));
-        HIP_TRY(hipMemcpyAsync(dst + db, d_dst, de - db, hipMemcpyDeviceToHost, P.d2h));
-        HIP_TRY(hipEventRecord(P.done[s], P.d2h));
         P.busy[s] = true;
+        if (unfinished >= 0 && (r = finish((uint32_t)unfinished))) return r;
+        unfinished = compact ? (int64_t)c : -1;
     }
-    if (packed && (r = finish(nchunks - 1))) return r;
+    if (unfinished >= 0 && (r = finish((uint32_t)unfinished))) return r;
+    // slot mode: the last compacted chunks' outputs to their dst_off, in chunk order
+    for (uint32_t k = 0; k < 2; k++) {
+        const uint32_t s = nchunks >= 2 ? (nchunks - 2 + k) & 1 : k;
+        if ((r = scatter(s))) return r;
+    }
     HIP_TRY(hipStreamSynchronize(P.d2h));
     P.busy[0] = P.busy[1] = false;
     return PMC_OK;
@@ -952,6 +1066,8 @@ int pinned_batch_run(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *
 int pinned_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
                  uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
                  int32_t *rc, uint32_t max_len, uint32_t chunk) {
+    if (!ctx) return PMC_E_ARG;
+    HostCall guard(ctx);
     const int r = pinned_batch_run(ctx, dir, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len,
                                    chunk);
     if (r && ctx && ctx->pipe.h2d) {

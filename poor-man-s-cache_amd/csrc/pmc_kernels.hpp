@@ -10,6 +10,7 @@ constexpr int PMC_INVALID_INPUT_DEV = -999;
 constexpr int PMC_Z_DATA_ERROR_DEV = -3;
 constexpr int PMC_Z_BUF_ERROR_DEV = -5;
 constexpr int PMC_E_CAPACITY_DEV = -101;
+constexpr int PMC_E_ARG_DEV = -102;
 
 constexpr uint32_t kSlabSyms = 16384; // per-wave symbol slab (>= 16383 symbols per block)
 
@@ -111,6 +112,8 @@ template <bool kHbm>
 __global__ void inflate_kernel(InflateArgs a);
 __global__ void inflate_lane_kernel(InflateArgs a);
 __global__ void inflate_verify_kernel(InflateArgs a);
+__global__ void arg_check_kernel(const uint32_t *src_len, uint64_t n, uint64_t max_len, int32_t *rc,
+                                 uint32_t *dst_len);
 __global__ void crc32_batch_kernel(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint64_t n,
                                    uint32_t *crc);
 

@@ -70,6 +70,18 @@ __global__ void compare_values_kernel(const uint8_t *a, const uint64_t *a_off, c
     if (l == 0 && bad) atomicAdd(mism, bad);
 }
 
+// The batch calls' argument check (include/pmc_codec.h): a value longer than the call's max_len
+// is claimed by no deflate variant, so it gets rc = PMC_E_ARG and dst_len = 0 here instead of
+// being left unwritten.
+__global__ void arg_check_kernel(const uint32_t *src_len, uint64_t n, uint64_t max_len, int32_t *rc,
+                                 uint32_t *dst_len) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        if (src_len[i] > max_len) {
+            rc[i] = PMC_E_ARG_DEV;
+            dst_len[i] = 0;
+        }
+}
+
 __global__ void isize_kernel(const uint8_t *src, const uint64_t *off, const uint32_t *len, uint32_t n, uint32_t *isz) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t L = len[i];

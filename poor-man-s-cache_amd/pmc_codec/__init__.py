@@ -97,6 +97,23 @@ def lib():
     return _lib
 
 
+def source_id() -> str:
+    """SHA-256 (16 hex) of the HIP library's sources (csrc/*.hip, csrc/*.hpp, include/pmc_codec.h):
+    stamps PMC-derived artifacts (profiles/*/traffic.json) so bench.py only quotes measurements
+    taken on the kernels it is running."""
+    import hashlib
+    pkg = os.path.dirname(HERE)
+    csrc = os.path.join(pkg, "csrc")
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".hip", ".hpp")))
+    files.append(os.path.join(os.path.dirname(pkg), "include", "pmc_codec.h"))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def last_error() -> str:
     return lib().pmc_last_error().decode()
 

@@ -347,28 +347,43 @@ def test_crc32_batch_vs_oracle(ctx, D):
     assert not bad, [(int(lens[i]), int(offs[i]) % 4) for i in bad[:10]]
 
 
-@pytest.mark.parametrize("chunk,packed", [(0, False), (1, False), (7, False), (64, False), (0, True), (1, True),
-                                          (7, True), (64, True)])
-def test_pinned_pipelined_batch_vs_oracle(ctx, golden, chunk, packed):
+@pytest.mark.parametrize("chunk", [0, 1, 7, 64])
+@pytest.mark.parametrize("mode", ["tiled", "scattered", "packed"])
+def test_pinned_pipelined_batch_vs_oracle(ctx, golden, chunk, mode):
     """pmc_gzip_{compress,decompress}_batch_pinned: ragged golden values (1 B .. 82 KB, LDS and HBM
     kernel variants in one batch) in pinned host buffers with gaps between values, cut into chunks
     whose copies overlap the neighbouring chunks' kernels; bit-exact vs the goldens and an exact
-    round trip.  Slot mode: outputs at dst_off, bytes past every chunk's slot range untouched.
-    Packed mode (dst_off NULL): outputs back to back in index order, failed values taking no bytes."""
+    round trip.  tiled: slots back to back in index order (whole ranges copied back), bytes past the
+    last slot untouched.  scattered: permuted slots with gaps (chunk ranges interleave),
+    and no byte outside a successful value's [dst_off, dst_off + dst_len) may change.  packed
+    (dst_off NULL): outputs back to back in index order, failed values taking no bytes."""
     import torch
+    packed, scattered = mode == "packed", mode == "scattered"
     pairs = [(r, g) for r, g in golden.pairs() if r][:300]
-    if packed:
-        pairs.insert(5, (b"\x00" * 40, None))  # placeholder slot made to fail below (cap too small)
+    pairs.insert(5, (b"\x00" * 40, None))  # a value made to fail below (capacity too small)
     n = len(pairs)
+    rng = np.random.default_rng(chunk * 3 + len(mode))
     lens = np.array([len(r) for r, _ in pairs], dtype=np.int64)
-    gaps = np.random.default_rng(chunk).integers(0, 5, n)
+    gaps = rng.integers(0, 5, n)
     soff = np.cumsum(np.concatenate([[3], (lens + gaps)[:-1]]))
     src = torch.zeros(int(soff[-1] + lens[-1] + 64), dtype=torch.uint8).pin_memory()
     for k, (r, _) in enumerate(pairs):
         src[int(soff[k]):int(soff[k]) + len(r)] = torch.frombuffer(bytearray(r), dtype=torch.uint8)
     caps = np.array([len(g) + 40 if g is not None else 8 for _, g in pairs], dtype=np.int64)
-    doff = np.concatenate([[0], np.cumsum(caps)[:-1]])
-    dst = torch.full((int(caps.sum()) + 64,), 0xEE, dtype=torch.uint8).pin_memory()
+
+    def slots(sizes):
+        """tiled: back to back in index order; scattered: permuted order, 0..9 B gaps."""
+        if not scattered:
+            return np.concatenate([[0], np.cumsum(sizes)[:-1]]), int(sizes.sum())
+        perm = rng.permutation(len(sizes))
+        g = rng.integers(0, 10, len(sizes))
+        pos = np.cumsum(np.concatenate([[7], (sizes[perm] + g[perm])[:-1]]))
+        off = np.empty(len(sizes), np.int64)
+        off[perm] = pos
+        return off, int(pos[-1] + sizes[perm[-1]] + 16)
+
+    doff, dsize = slots(caps)
+    dst = torch.full((dsize + 64,), 0xEE, dtype=torch.uint8).pin_memory()
     pin = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).pin_memory()  # noqa: E731
     t_soff, t_slen = pin(soff, np.int64), pin(lens, np.int32)
     t_doff, t_dcap = pin(doff, np.int64), pin(caps, np.int32)
@@ -385,14 +400,22 @@ def test_pinned_pipelined_batch_vs_oracle(ctx, golden, chunk, packed):
     raw = dst.numpy().tobytes()
     bad = [k for k, (_, g) in enumerate(pairs) if g is not None and raw[doff[k]:doff[k] + int(dlen[k])] != g]
     assert not bad, bad[:10]
-    end = int(got_len.sum()) if packed else len(raw) - 64
-    assert raw[end:] == b"\xee" * (len(raw) - end)
-    # decompress the good members where they lie into a fresh ragged buffer
+    if scattered:
+        # chunks of >= 2 permuted slots are compacted: every byte outside the successful outputs is
+        # untouched; a one-value chunk is a tiled range (its slot may be written whole)
+        mask = np.ones(len(raw), bool)
+        for k in range(n):
+            mask[doff[k]:doff[k] + (caps[k] if chunk == 1 else got_len[k])] = False
+        assert (dst.numpy()[mask] == 0xEE).all()
+    else:
+        end = int(got_len.sum()) if packed else len(raw) - 64
+        assert raw[end:] == b"\xee" * (len(raw) - end)
+    # decompress the good members where they lie into a fresh buffer (same layout kind)
     keep = np.nonzero(ok)[0]
     m_off, m_len = pin(doff[keep], np.int64), pin(got_len[keep], np.int32)
     vlens = lens[keep]
-    boff = np.concatenate([[5], 5 + np.cumsum(vlens + 3)[:-1]])
-    back = torch.zeros(int(boff[-1] + vlens[-1] + 64), dtype=torch.uint8).pin_memory()
+    boff, bsize = slots(vlens)
+    back = torch.full((bsize + 64,), 0x5A, dtype=torch.uint8).pin_memory()
     blen = torch.zeros(len(keep), dtype=torch.int32).pin_memory()
     brc = torch.full((len(keep),), 7, dtype=torch.int32).pin_memory()
     ctx.decompress_pinned(dst, m_off, m_len, back, None if packed else pin(boff, np.int64), pin(vlens, np.int32),
@@ -404,6 +427,36 @@ def test_pinned_pipelined_batch_vs_oracle(ctx, golden, chunk, packed):
     bad = [j for j, k in enumerate(keep)
            if int(blen[j]) != len(pairs[k][0]) or braw[boff[j]:boff[j] + vlens[j]] != pairs[k][0]]
     assert not bad, bad[:10]
+    if scattered:
+        mask = np.ones(len(braw), bool)
+        for j in range(len(keep)):
+            mask[boff[j]:boff[j] + vlens[j]] = False  # decompress capacities are the exact sizes
+        assert (back.numpy()[mask] == 0x5A).all()
+
+
+def test_compress_max_len_below_value_is_arg_error(ctx, D, golden):
+    """A value longer than the call's max_len is claimed by no kernel variant: it must come back
+    rc = PMC_E_ARG with dst_len 0 (device-side check), its neighbours compressed as usual; for a
+    max_len in the LDS range and one in the HBM range."""
+    import torch
+    pairs = [(r, g) for r, g in golden.pairs() if r]
+    for max_len in (300, 20000):
+        sel = [(r, g) for r, g in pairs if len(r) <= 40000][:200]
+        b = D.pack([r for r, _ in sel])
+        n = len(sel)
+        cap = torch.full((n,), 120000, dtype=torch.int32, device="cuda")
+        off = torch.arange(n, dtype=torch.int64, device="cuda") * 120000
+        out = torch.full((n * 120000,), 0xEE, dtype=torch.uint8, device="cuda")
+        dlen = torch.full((n,), 12345, dtype=torch.int32, device="cuda")
+        rc = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+        ctx.compress_device(b.data, b.off, b.len, out, off, cap, dlen, rc, max_len, D.stream_handle())
+        sync()
+        rcn, dl, o = rc.cpu().numpy(), dlen.cpu().numpy(), out.cpu().numpy()
+        for k, (r, g) in enumerate(sel):
+            if len(r) > max_len:
+                assert rcn[k] == -102 and dl[k] == 0, (k, len(r), rcn[k], dl[k])
+            else:
+                assert rcn[k] == 0 and o[k * 120000:k * 120000 + dl[k]].tobytes() == g, (k, len(r), rcn[k])
 
 
 def test_scattered_slots_in_place_store(ctx, D, golden):
