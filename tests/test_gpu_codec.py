@@ -307,6 +307,24 @@ def test_route_keys_vs_oracle(ctx, D):
         assert g[i] == (L.oracle_murmur3_x64_128_h1(k, len(k), 0) % 128) % 8, i
 
 
+@pytest.mark.parametrize("first,n", [(0, 5000), (9_999_000, 2000), (79_999_000, 1000)])
+def test_route_keys_vs_reference_hash(ctx, D, first, n):
+    """pmc_route_keys against the reference's own hashFunc (tests/golden/route_golden.npz, made from
+    /root/reference/src/hash by make_route_golden.py): GPU = hash % 128 % nGPU for 1..8 GPUs."""
+    import torch
+    import pmc_codec
+    z = np.load(os.path.join(ROOT, "tests", "golden", "route_golden.npz"))
+    idx, h = z["index"], z["hash"]
+    sel = (idx >= first) & (idx < first + n)
+    assert sel.sum() == n
+    want_shard = h[sel] % np.uint64(128)
+    gpu = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    for g in range(1, 9):
+        assert pmc_codec.lib().pmc_route_keys(first, n, 128, g, gpu.data_ptr(), D.stream_handle()) == 0
+        sync()
+        assert (gpu.cpu().numpy() == (want_shard % np.uint64(g)).astype(np.uint8)).all(), g
+
+
 def test_host_batch_api(ctx, golden):
     from oracle import pyoracle as O
     vals = [r for r, _ in golden.pairs()[:40] if r]

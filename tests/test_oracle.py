@@ -6,6 +6,7 @@ CPU restatements -- the zlib-shaped one and the data-parallel-shaped one the HIP
 mirror -- must reproduce every byte; the oracle inflate must reproduce every verdict.
 """
 import hashlib
+import os
 import zlib
 
 import numpy as np
@@ -79,3 +80,16 @@ def test_bound_covers_worst_case():
     for n in (1, 29, 1024, 70000):
         b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         assert len(O.compress(b)) <= O.bound(n)
+
+
+def test_murmur_restatement_matches_reference_hash():
+    """oracle/util.c's MurmurHash3_x64_128 restatement (the checker of pmc_route_keys) equals the
+    reference's own hashFunc (hash.cpp:4-9) on every key of tests/golden/route_golden.npz."""
+    import ctypes
+    L = O.lib()
+    L.oracle_murmur3_x64_128_h1.restype = ctypes.c_uint64
+    L.oracle_murmur3_x64_128_h1.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32]
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "route_golden.npz"))
+    for i, h in zip(z["index"], z["hash"]):
+        k = b"key%d" % int(i)
+        assert L.oracle_murmur3_x64_128_h1(k, len(k), 0) == int(h), int(i)
