@@ -141,6 +141,50 @@ int pmc_gzip_decompress_batch_pinned(pmc_ctx *ctx, const uint8_t *src, const uin
                                      const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
                                      uint32_t chunk);
 
+/* ---- device-resident compressed value store -----------------------
+ * Keeps the compressed bytes of cache values in HBM instead of host memory: the reference's
+ * Entry.value of a compressed entry (/root/reference/src/kvs/kvs.hpp:38-44, filled at
+ * kvs.cpp:185-187) becomes a pmc_extent, an extent of one device heap.  The caller keeps its own
+ * key index (the reference's hash table stays on the host) and stores the extent in it.
+ *   put: values (host memory) -> pinned staging -> H2D -> compress straight into freshly
+ *        allocated extents (gzip_bound(len) rounded to 16 B) -> only lengths come back.
+ *   get: extents -> decompress on the device into a packed response image, optionally framed
+ *        as the server's wire format (f3: the custom protocol's value + 0x1F, or a RESP bulk
+ *        string "$<len>\r\n<value>\r\n", /root/reference/src/server/protocol.cpp:399-406,
+ *        466-497) -> one D2H into the store's pinned buffer; resp[i] points into it (valid
+ *        until the next get on this store), ready for sendmsg without another copy.
+ *   free: extents return to the store's free lists (size classes).
+ * Calls are synchronous (return after the device work completed) and lock the store. */
+typedef struct pmc_store pmc_store;
+typedef struct pmc_extent {
+    uint64_t off;     /* byte offset in the store's device heap */
+    uint32_t cap;     /* bytes reserved */
+    uint32_t len;     /* compressed (gzip member) bytes */
+    uint32_t raw_len; /* value bytes (the member's ISIZE) */
+    uint32_t flags;   /* 0 = empty, 1 = live */
+} pmc_extent;
+#define PMC_FRAME_RAW 0    /* the value bytes only                                       */
+#define PMC_FRAME_CUSTOM 1 /* value + 0x1F (custom protocol response, protocol.hpp:17)   */
+#define PMC_FRAME_RESP 2   /* "$<len>\r\n" value "\r\n" (RESP bulk string)               */
+/* heap_bytes: device heap size (the extents live here; 0 = 1 GiB). */
+int pmc_store_create(pmc_ctx *ctx, uint64_t heap_bytes, pmc_store **out);
+void pmc_store_destroy(pmc_store *s);
+/* Compress value i (src + src_off[i], src_len[i] bytes, host memory) into a new extent:
+ * ext[i] (flags 1) and rc[i] = 0, or rc[i] = PMC_Z_MEM_ERROR (heap full) / a codec code with
+ * ext[i].flags = 0.  Returns PMC_OK unless the call itself failed. */
+int pmc_store_put_batch(pmc_store *s, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                        uint32_t n, pmc_extent *ext, int32_t *rc);
+/* Decompress extents into framed responses (frame = PMC_FRAME_*): resp[i], resp_len[i], rc[i]. */
+int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n, int frame, const uint8_t **resp,
+                        uint32_t *resp_len, int32_t *rc);
+/* Copy extents' compressed bytes (gzip members) to host memory: member i at dst + dst_off[i]. */
+int pmc_store_read_members(pmc_store *s, const pmc_extent *ext, uint32_t n, uint8_t *dst,
+                           const uint64_t *dst_off);
+/* Release extents (flags set to 0); freeing an empty extent is a no-op. */
+int pmc_store_free(pmc_store *s, pmc_extent *ext, uint32_t n);
+/* used: bytes held by live extents; reserved: heap bytes handed out so far; heap: heap size. */
+int pmc_store_stats(pmc_store *s, uint64_t *used, uint64_t *reserved, uint64_t *heap);
+
 /* ---- benchmark / test helpers (device, enqueue only) -----------------------------------
  * Synthetic values of SURVEY.md §8d: value i of vlen bytes written to dst + i*vlen, with
  * global index idx = index ? index[i] : first+i.  kind 0 = slice of corpus at

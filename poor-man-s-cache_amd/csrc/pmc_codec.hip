@@ -7,3 +7,4 @@
 #include "pmc_inflate_lane.hip"
 #include "pmc_misc.hip"
 #include "pmc_capi.hip"
+#include "pmc_store.hip"

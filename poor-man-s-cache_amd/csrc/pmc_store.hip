@@ -1,0 +1,341 @@
+// pmc_store.hip -- device-resident compressed value store (include/pmc_codec.h).
+//
+// The reference keeps every compressed value in host memory: Entry.value holds the gzip member
+// that insertEntry got from GzipCompressor::Compress (/root/reference/src/kvs/kvs.cpp:183-187,
+// kvs.hpp:38-44), a >= 16 KiB new[] buffer per value (gzip_compressor.cpp:21-33), and every GET
+// decompresses it into another new[] buffer (kvs.cpp:233) that the response then copies again
+// (protocol.cpp:466-497).  Here the members live in one HBM heap:
+//   * a SET batch crosses PCIe once as raw values and is compressed straight into its extents;
+//   * a GET batch is decompressed on the device into the packed response image of the batch,
+//     which crosses PCIe once into a pinned buffer; the wire framing (custom protocol's 0x1F or a
+//     RESP bulk string header/trailer) is written around each value in that buffer, so the value
+//     bytes are never copied on the host (f3).
+// The heap allocator is host-side: extents of gzip_bound(len) rounded to 16 B (to 1/8 of a power of
+// two above 8 KiB), per-size free lists, bump allocation otherwise.  Compiled into the unity TU after
+// pmc_capi.hip (uses pmc_ctx, DevBuf, HostBuf, the scan/compact kernels).
+
+#include <unordered_map>
+
+struct pmc_store {
+    pmc_ctx *ctx = nullptr;
+    std::mutex mu;
+    DevBuf heap;
+    uint64_t heap_bytes = 0, bump = 0, used = 0;
+    std::unordered_map<uint32_t, std::vector<uint64_t>> free_lists;  // extent size -> offsets
+    DevBuf dstage;   // device side of a call: arrays + value bytes / response image
+    HostBuf hstage;  // pinned host side of put / read_members
+    HostBuf hresp;   // pinned response image of the last get (resp[] points here)
+};
+
+namespace {
+
+uint32_t extent_size(uint64_t len) {
+    uint64_t c = (gzip_bound(len) + 15) & ~(uint64_t)15;
+    if (c > 8192) {
+        uint64_t p = 1;
+        while (p * 2 <= c) p *= 2;
+        const uint64_t step = p / 8;
+        c = (c + step - 1) / step * step;
+    }
+    return (uint32_t)c;
+}
+
+bool store_alloc(pmc_store *s, uint32_t size, uint64_t *off) {
+    auto it = s->free_lists.find(size);
+    if (it != s->free_lists.end() && !it->second.empty()) {
+        *off = it->second.back();
+        it->second.pop_back();
+    } else {
+        if (s->bump + size > s->heap_bytes) return false;
+        *off = s->bump;
+        s->bump += size;
+    }
+    s->used += size;
+    return true;
+}
+
+void store_release(pmc_store *s, pmc_extent &e) {
+    if (!(e.flags & 1)) return;
+    s->free_lists[e.cap].push_back(e.off);
+    s->used -= e.cap;
+    e.flags = 0;
+}
+
+struct StoreCall {  // the store's lock + the caller's device restored afterwards
+    std::lock_guard<std::mutex> lock;
+    int prev = -1;
+    explicit StoreCall(pmc_store *s) : lock(s->mu) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(s->ctx->device);
+    }
+    ~StoreCall() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+inline uint64_t al256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
+
+} // namespace
+
+PMC_API int pmc_store_create(pmc_ctx *ctx, uint64_t heap_bytes, pmc_store **out) {
+    if (!out) return PMC_E_ARG;
+    *out = nullptr;
+    if (!ctx) return PMC_E_ARG;
+    if (heap_bytes == 0) heap_bytes = 1ull << 30;
+    HIP_TRY(hipSetDevice(ctx->device));
+    pmc_store *s = new pmc_store;
+    s->ctx = ctx;
+    if (int r = s->heap.ensure(heap_bytes)) {
+        delete s;
+        return r;
+    }
+    s->heap_bytes = heap_bytes;
+    *out = s;
+    return PMC_OK;
+}
+
+PMC_API void pmc_store_destroy(pmc_store *s) {
+    if (!s) return;
+    {
+        StoreCall call(s);
+        (void)hipStreamSynchronize(s->ctx->stream);
+        s->heap.release();
+        s->dstage.release();
+        s->hstage.release();
+        s->hresp.release();
+    }
+    delete s;
+}
+
+PMC_API int pmc_store_put_batch(pmc_store *s, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                                uint32_t n, pmc_extent *ext, int32_t *rc) {
+    if (!s || (n && (!src || !src_off || !src_len || !ext || !rc))) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    StoreCall call(s);
+    pmc_ctx *ctx = s->ctx;
+    // values sent to the codec: non-empty ones that got an extent
+    std::vector<uint32_t> pick;
+    pick.reserve(n);
+    uint64_t bytes = 0, max_len = 1;
+    for (uint32_t i = 0; i < n; i++) {
+        ext[i] = pmc_extent{0, 0, 0, 0, 0};
+        if (src_len[i] == 0) {
+            rc[i] = PMC_INVALID_INPUT;
+            continue;
+        }
+        const uint32_t size = extent_size(src_len[i]);
+        uint64_t off = 0;
+        if (!store_alloc(s, size, &off)) {
+            rc[i] = PMC_Z_MEM_ERROR;
+            continue;
+        }
+        ext[i] = pmc_extent{off, size, 0, src_len[i], 1};
+        rc[i] = PMC_OK;
+        pick.push_back(i);
+        bytes += src_len[i];
+        max_len = std::max<uint64_t>(max_len, src_len[i]);
+    }
+    const uint32_t m = (uint32_t)pick.size();
+    if (m == 0) return PMC_OK;
+    // staging: soff | doff (u64) | slen | dcap | dlen | rc (u32) | value bytes
+    const uint64_t meta = al256(m * 8ull) * 2 + al256(m * 4ull) * 4;
+    int r = s->hstage.ensure(meta + bytes + 64);
+    if (!r) r = s->dstage.ensure(meta + bytes + 64);
+    if (r) {
+        for (uint32_t k = 0; k < m; k++) {
+            store_release(s, ext[pick[k]]);
+            rc[pick[k]] = r;
+        }
+        return r;
+    }
+    uint8_t *hp = (uint8_t *)s->hstage.p, *dp = (uint8_t *)s->dstage.p;
+    uint64_t *h_soff = (uint64_t *)hp, *h_doff = (uint64_t *)(hp + al256(m * 8ull));
+    uint32_t *h_slen = (uint32_t *)(hp + al256(m * 8ull) * 2);
+    uint32_t *h_dcap = (uint32_t *)((uint8_t *)h_slen + al256(m * 4ull));
+    uint32_t *h_dlen = (uint32_t *)((uint8_t *)h_dcap + al256(m * 4ull));
+    int32_t *h_rc = (int32_t *)((uint8_t *)h_dlen + al256(m * 4ull));
+    uint8_t *h_src = hp + meta;
+    const uint64_t d_base = (uint64_t)(dp - hp);  // device address = host address + d_base
+    auto dev = [&](void *h) { return (uint8_t *)h + d_base; };
+    uint64_t so = 0;
+    for (uint32_t k = 0; k < m; k++) {
+        const uint32_t i = pick[k];
+        h_soff[k] = so;
+        h_slen[k] = src_len[i];
+        memcpy(h_src + so, src + src_off[i], src_len[i]);
+        so += src_len[i];
+        h_doff[k] = ext[i].off;
+        h_dcap[k] = ext[i].cap;
+    }
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(dp, hp, meta + bytes, hipMemcpyHostToDevice, st));
+    r = pmc_gzip_compress_batch(ctx, dev(h_src), (uint64_t *)dev(h_soff), (uint32_t *)dev(h_slen), m,
+                                (uint8_t *)s->heap.p, (uint64_t *)dev(h_doff), (uint32_t *)dev(h_dcap),
+                                (uint32_t *)dev(h_dlen), (int32_t *)dev(h_rc), (uint32_t)max_len, st);
+    if (!r) {
+        HIP_TRY(hipMemcpyAsync(h_dlen, dev(h_dlen), al256(m * 4ull) * 2, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    for (uint32_t k = 0; k < m; k++) {
+        const uint32_t i = pick[k];
+        const int code = r ? r : h_rc[k];
+        if (code != PMC_OK) {
+            store_release(s, ext[i]);
+            rc[i] = code;
+            continue;
+        }
+        ext[i].len = h_dlen[k];
+    }
+    return r;
+}
+
+PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n, int frame, const uint8_t **resp,
+                                uint32_t *resp_len, int32_t *rc) {
+    if (!s || (n && (!ext || !resp || !resp_len || !rc)) || frame < PMC_FRAME_RAW || frame > PMC_FRAME_RESP)
+        return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    StoreCall call(s);
+    pmc_ctx *ctx = s->ctx;
+    std::vector<uint32_t> pick;
+    std::vector<uint64_t> pos(n, 0);
+    std::vector<uint8_t> hlen(n, 0);
+    uint64_t total = 0, max_raw = 1;
+    auto digits = [](uint32_t v) {
+        uint32_t d = 1;
+        while (v >= 10) {
+            v /= 10;
+            d++;
+        }
+        return d;
+    };
+    const uint32_t tl = frame == PMC_FRAME_RESP ? 2 : frame == PMC_FRAME_CUSTOM ? 1 : 0;
+    for (uint32_t i = 0; i < n; i++) {
+        resp[i] = nullptr;
+        resp_len[i] = 0;
+        if (!(ext[i].flags & 1) || ext[i].len == 0) {
+            rc[i] = PMC_E_ARG;
+            continue;
+        }
+        hlen[i] = (uint8_t)(frame == PMC_FRAME_RESP ? 1 + digits(ext[i].raw_len) + 2 : 0);
+        pos[i] = total;
+        total += hlen[i] + (uint64_t)ext[i].raw_len + tl;
+        max_raw = std::max<uint64_t>(max_raw, ext[i].raw_len);
+        rc[i] = PMC_OK;
+        pick.push_back(i);
+    }
+    const uint32_t m = (uint32_t)pick.size();
+    if (m == 0) return PMC_OK;
+    // device staging: soff | doff (u64) | slen | dcap | dlen | rc (u32) | response image
+    const uint64_t meta = al256(m * 8ull) * 2 + al256(m * 4ull) * 4;
+    int r = s->hstage.ensure(meta);
+    if (!r) r = s->dstage.ensure(meta + total + 64);
+    if (!r) r = s->hresp.ensure(total + 64);
+    if (r) return r;
+    uint8_t *hp = (uint8_t *)s->hstage.p, *dp = (uint8_t *)s->dstage.p;
+    uint64_t *h_soff = (uint64_t *)hp, *h_doff = (uint64_t *)(hp + al256(m * 8ull));
+    uint32_t *h_slen = (uint32_t *)(hp + al256(m * 8ull) * 2);
+    uint32_t *h_dcap = (uint32_t *)((uint8_t *)h_slen + al256(m * 4ull));
+    uint32_t *h_dlen = (uint32_t *)((uint8_t *)h_dcap + al256(m * 4ull));
+    int32_t *h_rc = (int32_t *)((uint8_t *)h_dlen + al256(m * 4ull));
+    const uint64_t d_base = (uint64_t)(dp - hp);
+    auto dev = [&](void *h) { return (uint8_t *)h + d_base; };
+    for (uint32_t k = 0; k < m; k++) {
+        const uint32_t i = pick[k];
+        h_soff[k] = ext[i].off;
+        h_slen[k] = ext[i].len;
+        h_doff[k] = pos[i] + hlen[i];
+        h_dcap[k] = ext[i].raw_len;
+    }
+    hipStream_t st = ctx->stream;
+    uint8_t *d_img = dp + meta, *img = (uint8_t *)s->hresp.p;
+    HIP_TRY(hipMemcpyAsync(dp, hp, meta, hipMemcpyHostToDevice, st));
+    r = pmc_gzip_decompress_batch(ctx, (const uint8_t *)s->heap.p, (uint64_t *)dev(h_soff), (uint32_t *)dev(h_slen),
+                                  m, d_img, (uint64_t *)dev(h_doff), (uint32_t *)dev(h_dcap), (uint32_t *)dev(h_dlen),
+                                  (int32_t *)dev(h_rc), (uint32_t)max_raw, st);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(h_dlen, dev(h_dlen), al256(m * 4ull) * 2, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(img, d_img, total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (uint32_t k = 0; k < m; k++) {
+        const uint32_t i = pick[k];
+        if (h_rc[k] != PMC_OK || h_dlen[k] != ext[i].raw_len) {
+            rc[i] = h_rc[k] != PMC_OK ? h_rc[k] : PMC_Z_DATA_ERROR;
+            continue;
+        }
+        uint8_t *p = img + pos[i];
+        if (frame == PMC_FRAME_RESP) {  // "$<len>\r\n" value "\r\n"  (protocol.cpp:466-497)
+            const int nd = hlen[i] - 3;
+            p[0] = '$';
+            uint32_t v = ext[i].raw_len;
+            for (int d = nd; d >= 1; d--) {
+                p[d] = (uint8_t)('0' + v % 10);
+                v /= 10;
+            }
+            p[nd + 1] = '\r';
+            p[nd + 2] = '\n';
+            p[hlen[i] + ext[i].raw_len] = '\r';
+            p[hlen[i] + ext[i].raw_len + 1] = '\n';
+        } else if (frame == PMC_FRAME_CUSTOM) {  // value + MSG_SEPARATOR (protocol.hpp:17)
+            p[ext[i].raw_len] = 0x1F;
+        }
+        resp[i] = p;
+        resp_len[i] = hlen[i] + ext[i].raw_len + tl;
+    }
+    return PMC_OK;
+}
+
+PMC_API int pmc_store_read_members(pmc_store *s, const pmc_extent *ext, uint32_t n, uint8_t *dst,
+                                   const uint64_t *dst_off) {
+    if (!s || (n && (!ext || !dst || !dst_off))) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    StoreCall call(s);
+    for (uint32_t i = 0; i < n; i++)
+        if (!(ext[i].flags & 1)) return PMC_E_ARG;
+    // gather the members on the device (compact_kernel), then one D2H
+    const uint64_t meta = al256(n * 8ull) * 2 + al256(n * 4ull) * 2;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) total += ext[i].len;
+    int r = s->hstage.ensure(meta + total + 64);
+    if (!r) r = s->dstage.ensure(meta + total + 64);
+    if (r) return r;
+    uint8_t *hp = (uint8_t *)s->hstage.p, *dp = (uint8_t *)s->dstage.p;
+    uint64_t *h_soff = (uint64_t *)hp, *h_poff = (uint64_t *)(hp + al256(n * 8ull));
+    uint32_t *h_len = (uint32_t *)(hp + al256(n * 8ull) * 2);
+    int32_t *h_rc = (int32_t *)((uint8_t *)h_len + al256(n * 4ull));
+    const uint64_t d_base = (uint64_t)(dp - hp);
+    auto dev = [&](void *h) { return (uint8_t *)h + d_base; };
+    uint64_t p = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        h_soff[i] = ext[i].off;
+        h_poff[i] = p;
+        h_len[i] = ext[i].len;
+        h_rc[i] = 0;
+        p += ext[i].len;
+    }
+    hipStream_t st = s->ctx->stream;
+    HIP_TRY(hipMemcpyAsync(dp, hp, meta, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(compact_kernel, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0, st,
+                       (const uint8_t *)s->heap.p, (const uint64_t *)dev(h_soff), (const uint32_t *)dev(h_len),
+                       (const int32_t *)dev(h_rc), (const uint64_t *)dev(h_poff), n, dp + meta);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(hp + meta, dp + meta, total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < n; i++) memcpy(dst + dst_off[i], hp + meta + h_poff[i], ext[i].len);
+    return PMC_OK;
+}
+
+PMC_API int pmc_store_free(pmc_store *s, pmc_extent *ext, uint32_t n) {
+    if (!s || (n && !ext)) return PMC_E_ARG;
+    std::lock_guard<std::mutex> lock(s->mu);
+    for (uint32_t i = 0; i < n; i++) store_release(s, ext[i]);
+    return PMC_OK;
+}
+
+PMC_API int pmc_store_stats(pmc_store *s, uint64_t *used, uint64_t *reserved, uint64_t *heap) {
+    if (!s) return PMC_E_ARG;
+    std::lock_guard<std::mutex> lock(s->mu);
+    if (used) *used = s->used;
+    if (reserved) *reserved = s->bump;
+    if (heap) *heap = s->heap_bytes;
+    return PMC_OK;
+}

@@ -60,6 +60,13 @@ SIGNATURES = {
     "pmc_gzip_decompress_batch_host": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p]),
     "pmc_gzip_compress_batch_pinned": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p, _u32, _u32]),
     "pmc_gzip_decompress_batch_pinned": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p, _p, _p, _p, _u32, _u32]),
+    "pmc_store_create": (_c.c_int, [_p, _u64, _c.POINTER(_p)]),
+    "pmc_store_destroy": (None, [_p]),
+    "pmc_store_put_batch": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p]),
+    "pmc_store_get_batch": (_c.c_int, [_p, _p, _u32, _c.c_int, _p, _p, _p]),
+    "pmc_store_read_members": (_c.c_int, [_p, _p, _u32, _p, _p]),
+    "pmc_store_free": (_c.c_int, [_p, _p, _u32]),
+    "pmc_store_stats": (_c.c_int, [_p, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_u64)]),
     "pmc_gen_values": (_c.c_int, [_p, _u32, _u64, _c.c_int, _u64, _p, _u32, _u32, _p, _p]),
     "pmc_fill_layout": (_c.c_int, [_p, _p, _p, _u32, _u64, _u32, _u32, _p]),
     "pmc_compare_values": (_c.c_int, [_p, _p, _p, _p, _p, _p, _u32, _p, _p]),
@@ -256,6 +263,89 @@ def default_context() -> Context:
     if _default is None:
         _default = Context(0)
     return _default
+
+
+# ------------------------------------------------------------ device-resident store (f2/f3)
+class Extent(ctypes.Structure):
+    """pmc_extent (include/pmc_codec.h)."""
+    _fields_ = [("off", _u64), ("cap", _u32), ("len", _u32), ("raw_len", _u32), ("flags", _u32)]
+
+
+FRAME_RAW, FRAME_CUSTOM, FRAME_RESP = 0, 1, 2
+
+
+class Store:
+    """Compressed values kept in an HBM heap: put(values) -> extents, get(extents, frame) -> responses."""
+
+    def __init__(self, ctx: Context, heap_bytes: int = 0):
+        self.ctx = ctx
+        self.handle = _p()
+        rc = lib().pmc_store_create(ctx.handle, heap_bytes, ctypes.byref(self.handle))
+        if rc != 0:
+            raise CodecUnavailable(f"pmc_store_create = {rc}: {last_error()}")
+
+    def put(self, values):
+        """values: list of bytes -> (Extent array, rc list)."""
+        import numpy as np
+        n = len(values)
+        ext = (Extent * max(n, 1))()
+        rc = np.zeros(max(n, 1), dtype=np.int32)
+        if n:
+            lens = np.array([len(v) for v in values], dtype=np.uint32)
+            off = np.zeros(n, dtype=np.uint64)
+            off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+            r = lib().pmc_store_put_batch(self.handle, b"".join(values), off.ctypes.data, lens.ctypes.data, n,
+                                          ext, rc.ctypes.data)
+            if r != 0:
+                raise CodecUnavailable(f"pmc_store_put_batch = {r}: {last_error()}")
+        return ext, [int(x) for x in rc[:n]]
+
+    def get(self, ext, n=None, frame=FRAME_RAW):
+        """-> list of (rc, response bytes)."""
+        import numpy as np
+        n = len(ext) if n is None else n
+        if n == 0:
+            return []
+        resp = (_p * n)()
+        rlen = np.zeros(n, dtype=np.uint32)
+        rc = np.zeros(n, dtype=np.int32)
+        r = lib().pmc_store_get_batch(self.handle, ext, n, frame, resp, rlen.ctypes.data, rc.ctypes.data)
+        if r != 0:
+            raise CodecUnavailable(f"pmc_store_get_batch = {r}: {last_error()}")
+        return [(int(rc[i]), ctypes.string_at(resp[i], int(rlen[i])) if rc[i] == 0 else b"") for i in range(n)]
+
+    def members(self, ext, n=None):
+        import numpy as np
+        n = len(ext) if n is None else n
+        lens = [ext[i].len for i in range(n)]
+        off = np.zeros(max(n, 1), dtype=np.uint64)
+        if n > 1:
+            off[1:n] = np.cumsum(lens[:-1], dtype=np.uint64)
+        buf = ctypes.create_string_buffer(sum(lens) + 1)
+        r = lib().pmc_store_read_members(self.handle, ext, n, buf, off.ctypes.data)
+        if r != 0:
+            raise CodecUnavailable(f"pmc_store_read_members = {r}: {last_error()}")
+        raw = buf.raw
+        return [raw[int(off[i]):int(off[i]) + lens[i]] for i in range(n)]
+
+    def free(self, ext, n=None):
+        lib().pmc_store_free(self.handle, ext, len(ext) if n is None else n)
+
+    def stats(self):
+        u, r, h = _u64(), _u64(), _u64()
+        lib().pmc_store_stats(self.handle, ctypes.byref(u), ctypes.byref(r), ctypes.byref(h))
+        return {"used": u.value, "reserved": r.value, "heap": h.value}
+
+    def close(self):
+        if self.handle:
+            lib().pmc_store_destroy(self.handle)
+            self.handle = _p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # ------------------------------------------------------------ reference mirror
