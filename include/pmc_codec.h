@@ -185,6 +185,30 @@ int pmc_store_free(pmc_store *s, pmc_extent *ext, uint32_t n);
 /* used: bytes held by live extents; reserved: heap bytes handed out so far; heap: heap size. */
 int pmc_store_stats(pmc_store *s, uint64_t *used, uint64_t *reserved, uint64_t *heap);
 
+/* ---- several GPUs from one process -----------------------------------------
+ * The reference server is one process that routes key k to shard hashFunc(k) % numShards
+ * (/root/reference/src/server/server.cpp:113,121,132).  A group holds one context per entry of
+ * `devices` (entries may repeat: two contexts on one GPU behave like two GPUs); value i of a group
+ * batch goes to member (key_hash[i] % num_shards) % n, each member's share runs through its own
+ * context's pinned pipelined call on its own host thread, and outputs land at dst_off[i] in the
+ * caller's order.  All pointers are host memory (any, not necessarily pinned).  No collective. */
+typedef struct pmc_group pmc_group;
+/* hashFunc(key) of the reference: MurmurHash3_x64_128(key, len, seed 0)[0] (hash.cpp:4-9). */
+uint64_t pmc_key_hash(const void *key, size_t len);
+int pmc_group_create(const int *devices, int n, pmc_group **out);
+void pmc_group_destroy(pmc_group *g);
+int pmc_group_size(pmc_group *g);
+/* member[i] = (key_hash[i] % num_shards) % pmc_group_size(g) */
+int pmc_group_route(pmc_group *g, const uint64_t *key_hash, uint32_t num_shards, uint32_t n, uint32_t *member);
+int pmc_group_compress_batch(pmc_group *g, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                             const uint64_t *key_hash, uint32_t num_shards, uint32_t n, uint8_t *dst,
+                             const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc,
+                             uint32_t max_len);
+int pmc_group_decompress_batch(pmc_group *g, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                               const uint64_t *key_hash, uint32_t num_shards, uint32_t n, uint8_t *dst,
+                               const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc,
+                               uint32_t max_len);
+
 /* ---- benchmark / test helpers (device, enqueue only) -----------------------------------
  * Synthetic values of SURVEY.md §8d: value i of vlen bytes written to dst + i*vlen, with
  * global index idx = index ? index[i] : first+i.  kind 0 = slice of corpus at

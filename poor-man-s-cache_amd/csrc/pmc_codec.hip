@@ -8,3 +8,4 @@
 #include "pmc_misc.hip"
 #include "pmc_capi.hip"
 #include "pmc_store.hip"
+#include "pmc_group.hip"

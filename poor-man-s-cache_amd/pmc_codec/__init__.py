@@ -67,6 +67,13 @@ SIGNATURES = {
     "pmc_store_read_members": (_c.c_int, [_p, _p, _u32, _p, _p]),
     "pmc_store_free": (_c.c_int, [_p, _p, _u32]),
     "pmc_store_stats": (_c.c_int, [_p, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_u64)]),
+    "pmc_key_hash": (_u64, [_c.c_char_p, _c.c_size_t]),
+    "pmc_group_create": (_c.c_int, [_c.POINTER(_c.c_int), _c.c_int, _c.POINTER(_p)]),
+    "pmc_group_destroy": (None, [_p]),
+    "pmc_group_size": (_c.c_int, [_p]),
+    "pmc_group_route": (_c.c_int, [_p, _p, _u32, _u32, _p]),
+    "pmc_group_compress_batch": (_c.c_int, [_p, _p, _p, _p, _p, _u32, _u32, _p, _p, _p, _p, _p, _u32]),
+    "pmc_group_decompress_batch": (_c.c_int, [_p, _p, _p, _p, _p, _u32, _u32, _p, _p, _p, _p, _p, _u32]),
     "pmc_gen_values": (_c.c_int, [_p, _u32, _u64, _c.c_int, _u64, _p, _u32, _u32, _p, _p]),
     "pmc_fill_layout": (_c.c_int, [_p, _p, _p, _u32, _u64, _u32, _u32, _p]),
     "pmc_compare_values": (_c.c_int, [_p, _p, _p, _p, _p, _p, _u32, _p, _p]),

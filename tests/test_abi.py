@@ -68,3 +68,21 @@ def test_pinned_batch_rejects_bad_arguments_without_touching_a_device():
     for fn in (L.pmc_gzip_compress_batch_pinned, L.pmc_gzip_decompress_batch_pinned):
         assert fn(None, buf, buf, buf, 1, buf, None, buf, buf, buf, 16, 0) == pmc_codec.E_ARG
         assert fn(None, None, None, None, 0, None, None, None, None, None, 0, 0) == pmc_codec.E_ARG
+
+
+def test_host_key_hash_matches_reference_hash():
+    """pmc_key_hash (host side of the group route) equals the reference's own hashFunc
+    (tests/golden/route_golden.npz, from /root/reference/src/hash) -- a host function, no device."""
+    import numpy as np
+    z = np.load(os.path.join(ROOT, "tests", "golden", "route_golden.npz"))
+    L = pmc_codec.lib()
+    for i, h in zip(z["index"], z["hash"]):
+        k = b"key%d" % int(i)
+        assert L.pmc_key_hash(k, len(k)) == int(h), int(i)
+    # every tail length 0..15 and a few full blocks, against the oracle's restatement
+    from oracle import pyoracle as O
+    O.lib().oracle_murmur3_x64_128_h1.restype = ctypes.c_uint64
+    O.lib().oracle_murmur3_x64_128_h1.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32]
+    for n in range(0, 70):
+        k = bytes((7 * j + 3) % 251 + 1 for j in range(n))
+        assert L.pmc_key_hash(k, n) == O.lib().oracle_murmur3_x64_128_h1(k, n, 0), n
