@@ -1,0 +1,229 @@
+// pmc_loadgen.cpp -- pipelined custom-protocol load against pmc_server (or any server speaking it).
+//
+// Shaped like the reference's load test in pipeline mode (/root/reference/tests/tcp_server_test.py
+// :158-244, `-p -b 100`): each connection writes batches of B commands joined by 0x1F and then reads
+// B responses; connections run on their own threads.  Unlike that test, whose values (`value{i}`,
+// <= 12 chars) never reach the codec, values here are JSON slices of the reference's
+// tests/data corpus (SURVEY §8d generator), so every SET compresses and every GET decompresses.
+//
+// usage: pmc_loadgen --port P --data DIR [--conns 16] [--keys 65536] [--vlen 4096] [--batch 100]
+//                    [--ops 200000] [--mix 50]       (percent of SETs in the timed phase)
+// Phases: preload (SET every key once, untimed), then --ops timed commands over random keys,
+// every GET checked against the last value SET for its key.  Prints one JSON line.
+#include <arpa/inet.h>
+#include <dirent.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct Opts {
+    int port = 9001, conns = 16, batch = 100, mix = 50;
+    uint64_t keys = 65536, vlen = 4096, ops = 200000;
+    std::string data;
+};
+
+std::string corpus;
+
+// value of key k at version v: a corpus slice (splitmix64(seed ^ i) % (len - V + 1))
+std::string value_of(uint64_t k, uint64_t v, uint64_t vlen) {
+    const uint64_t off = splitmix64(0x5EEDull ^ (k * 1000003ull + v)) % (corpus.size() - vlen + 1);
+    return corpus.substr(off, vlen);
+}
+
+int connect_to(int port) {
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)port);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (connect(fd, (sockaddr *)&a, sizeof a) != 0) {
+        close(fd);
+        return -1;
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    return fd;
+}
+
+bool send_all(int fd, const std::string &s) {
+    size_t o = 0;
+    while (o < s.size()) {
+        const ssize_t w = send(fd, s.data() + o, s.size() - o, MSG_NOSIGNAL);
+        if (w <= 0) return false;
+        o += (size_t)w;
+    }
+    return true;
+}
+
+// reads n responses (0x1F-terminated) into out
+bool recv_n(int fd, std::string &buf, size_t n, std::vector<std::string> &out) {
+    out.clear();
+    size_t pos = 0;
+    char tmp[1 << 16];
+    while (out.size() < n) {
+        const size_t e = buf.find('\x1f', pos);
+        if (e != std::string::npos) {
+            out.emplace_back(buf, pos, e - pos);
+            pos = e + 1;
+            continue;
+        }
+        buf.erase(0, pos);
+        pos = 0;
+        const ssize_t r = recv(fd, tmp, sizeof tmp, 0);
+        if (r <= 0) return false;
+        buf.append(tmp, (size_t)r);
+    }
+    buf.erase(0, pos);
+    return true;
+}
+
+struct Worker {
+    uint64_t ops = 0, sets = 0, gets = 0, bytes = 0, bad = 0;
+};
+
+} // namespace
+
+int main(int argc, char **argv) {
+    Opts o;
+    for (int i = 1; i + 1 < argc; i += 2) {
+        const std::string a = argv[i], v = argv[i + 1];
+        if (a == "--port") o.port = atoi(v.c_str());
+        else if (a == "--conns") o.conns = atoi(v.c_str());
+        else if (a == "--keys") o.keys = strtoull(v.c_str(), nullptr, 10);
+        else if (a == "--vlen") o.vlen = strtoull(v.c_str(), nullptr, 10);
+        else if (a == "--batch") o.batch = atoi(v.c_str());
+        else if (a == "--ops") o.ops = strtoull(v.c_str(), nullptr, 10);
+        else if (a == "--mix") o.mix = atoi(v.c_str());
+        else if (a == "--data") o.data = v;
+        else {
+            fprintf(stderr, "unknown option %s\n", a.c_str());
+            return 2;
+        }
+    }
+    std::vector<std::string> names;
+    if (DIR *d = opendir(o.data.c_str())) {
+        while (dirent *e = readdir(d)) {
+            std::string n = e->d_name;
+            if (n.size() > 5 && n.substr(n.size() - 5) == ".json") names.push_back(n);
+        }
+        closedir(d);
+    }
+    std::sort(names.begin(), names.end());
+    for (auto &n : names) {
+        std::ifstream f(o.data + "/" + n, std::ios::binary);
+        std::stringstream ss;
+        ss << f.rdbuf();
+        corpus += ss.str();
+    }
+    if (corpus.size() < o.vlen + 1) {
+        fprintf(stderr, "corpus too small (%zu B from %s)\n", corpus.size(), o.data.c_str());
+        return 2;
+    }
+    // keys are owned by connections (key % conns), so each connection knows its keys' versions
+    std::vector<Worker> w(o.conns);
+    std::atomic<int> failed{0};
+    auto run_phase = [&](bool preload) {
+        std::vector<std::thread> th;
+        for (int c = 0; c < o.conns; c++)
+            th.emplace_back([&, c] {
+                const int fd = connect_to(o.port);
+                if (fd < 0) {
+                    failed++;
+                    return;
+                }
+                std::vector<uint64_t> mine;
+                for (uint64_t k = c; k < o.keys; k += o.conns) mine.push_back(k);
+                std::vector<uint64_t> ver(mine.size(), 0);
+                if (!preload) {  // versions after the preload
+                    for (auto &v : ver) v = 1;
+                }
+                uint64_t rng = splitmix64(0x7ull + c), todo = preload ? mine.size() : o.ops / o.conns, done = 0;
+                std::string buf, req;
+                std::vector<std::string> resp;
+                std::vector<std::pair<int, std::string>> expect;  // 0 = SET (OK), 1 = GET (value)
+                Worker &me = w[c];
+                while (done < todo) {
+                    req.clear();
+                    expect.clear();
+                    const uint64_t b = std::min<uint64_t>(o.batch, todo - done);
+                    for (uint64_t j = 0; j < b; j++) {
+                        size_t ki;
+                        bool set;
+                        if (preload) {
+                            ki = done + j;
+                            set = true;
+                        } else {
+                            rng = splitmix64(rng);
+                            ki = rng % mine.size();
+                            set = (int)((rng >> 40) % 100) < o.mix;
+                        }
+                        const uint64_t k = mine[ki];
+                        if (set) {
+                            const std::string v = value_of(k, ++ver[ki], o.vlen);
+                            req += "SET key" + std::to_string(k) + " " + v + '\x1f';
+                            expect.emplace_back(0, "OK");
+                            me.sets++;
+                        } else {
+                            req += "GET key" + std::to_string(k) + '\x1f';
+                            expect.emplace_back(1, value_of(k, ver[ki], o.vlen));
+                            me.gets++;
+                        }
+                        me.bytes += o.vlen;
+                    }
+                    if (!send_all(fd, req) || !recv_n(fd, buf, b, resp)) {
+                        failed++;
+                        break;
+                    }
+                    for (uint64_t j = 0; j < b; j++)
+                        if (resp[j] != expect[j].second) me.bad++;
+                    done += b;
+                    me.ops += b;
+                }
+                close(fd);
+            });
+        for (auto &t : th) t.join();
+    };
+    run_phase(true);
+    for (auto &x : w) x = Worker{};
+    const auto t0 = std::chrono::steady_clock::now();
+    run_phase(false);
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    Worker s;
+    for (auto &x : w) {
+        s.ops += x.ops;
+        s.sets += x.sets;
+        s.gets += x.gets;
+        s.bytes += x.bytes;
+        s.bad += x.bad;
+    }
+    printf("{\"ops\": %llu, \"sets\": %llu, \"gets\": %llu, \"seconds\": %.4f, \"ops_per_s\": %.1f, "
+           "\"value_gib_s\": %.4f, \"mismatches\": %llu, \"failed_conns\": %d, \"conns\": %d, \"batch\": %d, "
+           "\"vlen\": %llu, \"keys\": %llu, \"set_pct\": %d}\n",
+           (unsigned long long)s.ops, (unsigned long long)s.sets, (unsigned long long)s.gets, t, s.ops / t,
+           s.bytes / t / (1ull << 30), (unsigned long long)s.bad, failed.load(), o.conns, o.batch,
+           (unsigned long long)o.vlen, (unsigned long long)o.keys, o.mix);
+    return (s.bad || failed) ? 1 : 0;
+}

@@ -1,0 +1,28 @@
+#!/bin/bash
+# Loopback ops/s of pmc_server (BASELINE configs[4] shape: pipelined batches of 100
+# commands per connection) with the device store (--codec batch) against the per-value drop-in
+# path (--codec single, what the unchanged server does through GzipCompressor) and no codec.
+#   OUT=gpurun_out/x bash scripts/server_bench.sh
+cd "$GRAFT_REPO_ROOT" || cd "$(dirname "$0")/.." || exit 1
+OUT=${OUT:-gpurun_out/server}
+mkdir -p "$OUT"
+B=poor-man-s-cache_amd/pmc_codec
+run() {  # codec vlen ops conns mix
+    local port=$((20000 + RANDOM % 20000))
+    $B/pmc_server --port $port --codec $1 --heap-mb 8192 > "$OUT/server_$1_$2_$4_$5.log" 2>&1 &
+    local pid=$!
+    sleep 1
+    timeout -k 5 200 $B/pmc_loadgen --port $port --data tests/golden/data --vlen $2 --ops $3 --conns $4 \
+        --keys 65536 --batch 100 --mix $5 | sed "s/^{/{\"codec\": \"$1\", /" | tee -a "$OUT/server_bench.jsonl"
+    local rc=${PIPESTATUS[0]}
+    kill $pid; wait $pid
+    return $rc
+}
+run off 4096 400000 16 50 &&
+run batch 4096 400000 16 50 &&
+run batch 4096 400000 64 50 &&
+run batch 4096 400000 64 0 &&
+run batch 4096 400000 64 100 &&
+run batch 1024 400000 64 50 &&
+run single 4096 20000 16 50 &&
+run single 1024 20000 16 50
