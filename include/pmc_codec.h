@@ -154,7 +154,9 @@ int pmc_gzip_decompress_batch_pinned(pmc_ctx *ctx, const uint8_t *src, const uin
  *        466-497) -> one D2H into the store's pinned buffer; resp[i] points into it (valid
  *        until the next get on this store), ready for sendmsg without another copy.
  *   free: extents return to the store's free lists (size classes).
- * Calls are synchronous (return after the device work completed) and lock the store. */
+ * Calls are synchronous (return after the device work completed).  A put and a get (or
+ * read_members) may run at the same time from two threads (compress and decompress streams,
+ * separate staging); two puts, or two gets, are serialized. */
 typedef struct pmc_store pmc_store;
 typedef struct pmc_extent {
     uint64_t off;     /* byte offset in the store's device heap */

@@ -16,15 +16,20 @@
 
 #include <unordered_map>
 
+// A put (compress, on the context's stream) and a get (decompress, on the store's own stream) may
+// run at the same time from two threads: each direction has its own lock and staging buffers; the
+// allocator has a third lock.  Extents a get reads are never ones a concurrent put writes (a put
+// only writes extents it allocates, and callers free extents only after their gets returned).
 struct pmc_store {
     pmc_ctx *ctx = nullptr;
-    std::mutex mu;
+    std::mutex put_mu, get_mu, alloc_mu;
+    hipStream_t gst = nullptr;  // get / read_members stream
     DevBuf heap;
     uint64_t heap_bytes = 0, bump = 0, used = 0;
     std::unordered_map<uint32_t, std::vector<uint64_t>> free_lists;  // extent size -> offsets
-    DevBuf dstage;   // device side of a call: arrays + value bytes / response image
-    HostBuf hstage;  // pinned host side of put / read_members
-    HostBuf hresp;   // pinned response image of the last get (resp[] points here)
+    DevBuf pdev, gdev;    // device side of a put / a get: arrays + value bytes / response image
+    HostBuf phost, ghost; // pinned host side of a put / the arrays of a get
+    HostBuf hresp;        // pinned response image of the last get (resp[] points here)
 };
 
 namespace {
@@ -40,7 +45,7 @@ uint32_t extent_size(uint64_t len) {
     return (uint32_t)c;
 }
 
-bool store_alloc(pmc_store *s, uint32_t size, uint64_t *off) {
+bool store_alloc(pmc_store *s, uint32_t size, uint64_t *off) {  // alloc_mu held
     auto it = s->free_lists.find(size);
     if (it != s->free_lists.end() && !it->second.empty()) {
         *off = it->second.back();
@@ -54,17 +59,17 @@ bool store_alloc(pmc_store *s, uint32_t size, uint64_t *off) {
     return true;
 }
 
-void store_release(pmc_store *s, pmc_extent &e) {
+void store_release(pmc_store *s, pmc_extent &e) {  // alloc_mu held
     if (!(e.flags & 1)) return;
     s->free_lists[e.cap].push_back(e.off);
     s->used -= e.cap;
     e.flags = 0;
 }
 
-struct StoreCall {  // the store's lock + the caller's device restored afterwards
+struct StoreCall {  // one direction's lock + the caller's device restored afterwards
     std::lock_guard<std::mutex> lock;
     int prev = -1;
-    explicit StoreCall(pmc_store *s) : lock(s->mu) {
+    StoreCall(pmc_store *s, std::mutex &mu) : lock(mu) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
         (void)hipSetDevice(s->ctx->device);
     }
@@ -89,6 +94,11 @@ PMC_API int pmc_store_create(pmc_ctx *ctx, uint64_t heap_bytes, pmc_store **out)
         delete s;
         return r;
     }
+    if (hipStreamCreateWithFlags(&s->gst, hipStreamNonBlocking) != hipSuccess) {
+        s->heap.release();
+        delete s;
+        return PMC_E_NO_DEVICE;
+    }
     s->heap_bytes = heap_bytes;
     *out = s;
     return PMC_OK;
@@ -97,12 +107,17 @@ PMC_API int pmc_store_create(pmc_ctx *ctx, uint64_t heap_bytes, pmc_store **out)
 PMC_API void pmc_store_destroy(pmc_store *s) {
     if (!s) return;
     {
-        StoreCall call(s);
+        std::lock_guard<std::mutex> g(s->get_mu);
+        StoreCall call(s, s->put_mu);
         (void)hipStreamSynchronize(s->ctx->stream);
+        (void)hipStreamSynchronize(s->gst);
         s->heap.release();
-        s->dstage.release();
-        s->hstage.release();
+        s->pdev.release();
+        s->gdev.release();
+        s->phost.release();
+        s->ghost.release();
         s->hresp.release();
+        (void)hipStreamDestroy(s->gst);
     }
     delete s;
 }
@@ -111,12 +126,13 @@ PMC_API int pmc_store_put_batch(pmc_store *s, const uint8_t *src, const uint64_t
                                 uint32_t n, pmc_extent *ext, int32_t *rc) {
     if (!s || (n && (!src || !src_off || !src_len || !ext || !rc))) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
-    StoreCall call(s);
+    StoreCall call(s, s->put_mu);
     pmc_ctx *ctx = s->ctx;
     // values sent to the codec: non-empty ones that got an extent
     std::vector<uint32_t> pick;
     pick.reserve(n);
     uint64_t bytes = 0, max_len = 1;
+    std::unique_lock<std::mutex> alloc(s->alloc_mu);
     for (uint32_t i = 0; i < n; i++) {
         ext[i] = pmc_extent{0, 0, 0, 0, 0};
         if (src_len[i] == 0) {
@@ -135,20 +151,22 @@ PMC_API int pmc_store_put_batch(pmc_store *s, const uint8_t *src, const uint64_t
         bytes += src_len[i];
         max_len = std::max<uint64_t>(max_len, src_len[i]);
     }
+    alloc.unlock();
     const uint32_t m = (uint32_t)pick.size();
     if (m == 0) return PMC_OK;
     // staging: soff | doff (u64) | slen | dcap | dlen | rc (u32) | value bytes
     const uint64_t meta = al256(m * 8ull) * 2 + al256(m * 4ull) * 4;
-    int r = s->hstage.ensure(meta + bytes + 64);
-    if (!r) r = s->dstage.ensure(meta + bytes + 64);
+    int r = s->phost.ensure(meta + bytes + 64);
+    if (!r) r = s->pdev.ensure(meta + bytes + 64);
     if (r) {
+        std::lock_guard<std::mutex> a(s->alloc_mu);
         for (uint32_t k = 0; k < m; k++) {
             store_release(s, ext[pick[k]]);
             rc[pick[k]] = r;
         }
         return r;
     }
-    uint8_t *hp = (uint8_t *)s->hstage.p, *dp = (uint8_t *)s->dstage.p;
+    uint8_t *hp = (uint8_t *)s->phost.p, *dp = (uint8_t *)s->pdev.p;
     uint64_t *h_soff = (uint64_t *)hp, *h_doff = (uint64_t *)(hp + al256(m * 8ull));
     uint32_t *h_slen = (uint32_t *)(hp + al256(m * 8ull) * 2);
     uint32_t *h_dcap = (uint32_t *)((uint8_t *)h_slen + al256(m * 4ull));
@@ -176,6 +194,7 @@ PMC_API int pmc_store_put_batch(pmc_store *s, const uint8_t *src, const uint64_t
         HIP_TRY(hipMemcpyAsync(h_dlen, dev(h_dlen), al256(m * 4ull) * 2, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
+    std::lock_guard<std::mutex> a(s->alloc_mu);
     for (uint32_t k = 0; k < m; k++) {
         const uint32_t i = pick[k];
         const int code = r ? r : h_rc[k];
@@ -194,7 +213,7 @@ PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n,
     if (!s || (n && (!ext || !resp || !resp_len || !rc)) || frame < PMC_FRAME_RAW || frame > PMC_FRAME_RESP)
         return PMC_E_ARG;
     if (n == 0) return PMC_OK;
-    StoreCall call(s);
+    StoreCall call(s, s->get_mu);
     pmc_ctx *ctx = s->ctx;
     std::vector<uint32_t> pick;
     std::vector<uint64_t> pos(n, 0);
@@ -227,11 +246,11 @@ PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n,
     if (m == 0) return PMC_OK;
     // device staging: soff | doff (u64) | slen | dcap | dlen | rc (u32) | response image
     const uint64_t meta = al256(m * 8ull) * 2 + al256(m * 4ull) * 4;
-    int r = s->hstage.ensure(meta);
-    if (!r) r = s->dstage.ensure(meta + total + 64);
+    int r = s->ghost.ensure(meta);
+    if (!r) r = s->gdev.ensure(meta + total + 64);
     if (!r) r = s->hresp.ensure(total + 64);
     if (r) return r;
-    uint8_t *hp = (uint8_t *)s->hstage.p, *dp = (uint8_t *)s->dstage.p;
+    uint8_t *hp = (uint8_t *)s->ghost.p, *dp = (uint8_t *)s->gdev.p;
     uint64_t *h_soff = (uint64_t *)hp, *h_doff = (uint64_t *)(hp + al256(m * 8ull));
     uint32_t *h_slen = (uint32_t *)(hp + al256(m * 8ull) * 2);
     uint32_t *h_dcap = (uint32_t *)((uint8_t *)h_slen + al256(m * 4ull));
@@ -246,7 +265,7 @@ PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n,
         h_doff[k] = pos[i] + hlen[i];
         h_dcap[k] = ext[i].raw_len;
     }
-    hipStream_t st = ctx->stream;
+    hipStream_t st = s->gst;
     uint8_t *d_img = dp + meta, *img = (uint8_t *)s->hresp.p;
     HIP_TRY(hipMemcpyAsync(dp, hp, meta, hipMemcpyHostToDevice, st));
     r = pmc_gzip_decompress_batch(ctx, (const uint8_t *)s->heap.p, (uint64_t *)dev(h_soff), (uint32_t *)dev(h_slen),
@@ -288,17 +307,17 @@ PMC_API int pmc_store_read_members(pmc_store *s, const pmc_extent *ext, uint32_t
                                    const uint64_t *dst_off) {
     if (!s || (n && (!ext || !dst || !dst_off))) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
-    StoreCall call(s);
+    StoreCall call(s, s->get_mu);
     for (uint32_t i = 0; i < n; i++)
         if (!(ext[i].flags & 1)) return PMC_E_ARG;
     // gather the members on the device (compact_kernel), then one D2H
     const uint64_t meta = al256(n * 8ull) * 2 + al256(n * 4ull) * 2;
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; i++) total += ext[i].len;
-    int r = s->hstage.ensure(meta + total + 64);
-    if (!r) r = s->dstage.ensure(meta + total + 64);
+    int r = s->ghost.ensure(meta + total + 64);
+    if (!r) r = s->gdev.ensure(meta + total + 64);
     if (r) return r;
-    uint8_t *hp = (uint8_t *)s->hstage.p, *dp = (uint8_t *)s->dstage.p;
+    uint8_t *hp = (uint8_t *)s->ghost.p, *dp = (uint8_t *)s->gdev.p;
     uint64_t *h_soff = (uint64_t *)hp, *h_poff = (uint64_t *)(hp + al256(n * 8ull));
     uint32_t *h_len = (uint32_t *)(hp + al256(n * 8ull) * 2);
     int32_t *h_rc = (int32_t *)((uint8_t *)h_len + al256(n * 4ull));
@@ -312,7 +331,7 @@ PMC_API int pmc_store_read_members(pmc_store *s, const pmc_extent *ext, uint32_t
         h_rc[i] = 0;
         p += ext[i].len;
     }
-    hipStream_t st = s->ctx->stream;
+    hipStream_t st = s->gst;
     HIP_TRY(hipMemcpyAsync(dp, hp, meta, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(compact_kernel, dim3(std::min<uint32_t>((n + 3) / 4, 8192)), dim3(256), 0, st,
                        (const uint8_t *)s->heap.p, (const uint64_t *)dev(h_soff), (const uint32_t *)dev(h_len),
@@ -326,14 +345,14 @@ PMC_API int pmc_store_read_members(pmc_store *s, const pmc_extent *ext, uint32_t
 
 PMC_API int pmc_store_free(pmc_store *s, pmc_extent *ext, uint32_t n) {
     if (!s || (n && !ext)) return PMC_E_ARG;
-    std::lock_guard<std::mutex> lock(s->mu);
+    std::lock_guard<std::mutex> lock(s->alloc_mu);
     for (uint32_t i = 0; i < n; i++) store_release(s, ext[i]);
     return PMC_OK;
 }
 
 PMC_API int pmc_store_stats(pmc_store *s, uint64_t *used, uint64_t *reserved, uint64_t *heap) {
     if (!s) return PMC_E_ARG;
-    std::lock_guard<std::mutex> lock(s->mu);
+    std::lock_guard<std::mutex> lock(s->alloc_mu);
     if (used) *used = s->used;
     if (reserved) *reserved = s->bump;
     if (heap) *heap = s->heap_bytes;

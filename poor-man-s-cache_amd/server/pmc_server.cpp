@@ -113,8 +113,10 @@ struct Gpu {
 
 struct Stats {
     uint64_t iterations = 0, requests = 0, sets = 0, gets = 0, dels = 0, compressed = 0, decompressed = 0,
-             raw_fallbacks = 0, pending_hits = 0;
+             raw_fallbacks = 0, pending_hits = 0, put_calls = 0, get_calls = 0;
+    double t_codec = 0, t_put = 0, t_get = 0, t_iter = 0;  // seconds: codec phase, store calls, whole iterations
 };
+double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
 class Server {
   public:
@@ -205,9 +207,14 @@ int Server::run(int port) {
             }
         }
         if (ready.empty()) continue;
+        const double t_it = now_s();
         // one batch: every complete request of every ready connection
         reqs.clear();
         arena.clear();
+        for (auto &g : gpus) {
+            g.puts.clear();
+            g.gets.clear();
+        }
         std::vector<std::pair<size_t, size_t>> span(ready.size());
         for (size_t j = 0; j < ready.size(); j++) {
             span[j].first = reqs.size();
@@ -227,13 +234,17 @@ int Server::run(int port) {
                 g.to_free.clear();
             }
         st.iterations++;
+        st.t_iter += now_s() - t_it;
     }
     printf("{\"iterations\": %llu, \"requests\": %llu, \"sets\": %llu, \"gets\": %llu, \"dels\": %llu, "
-           "\"compressed\": %llu, \"decompressed\": %llu, \"raw_fallbacks\": %llu, \"pending_hits\": %llu}\n",
+           "\"compressed\": %llu, \"decompressed\": %llu, \"raw_fallbacks\": %llu, \"pending_hits\": %llu, "
+           "\"put_calls\": %llu, \"get_calls\": %llu, \"t_iter\": %.4f, \"t_codec\": %.4f, \"t_put\": %.4f, "
+           "\"t_get\": %.4f}\n",
            (unsigned long long)st.iterations, (unsigned long long)st.requests, (unsigned long long)st.sets,
            (unsigned long long)st.gets, (unsigned long long)st.dels, (unsigned long long)st.compressed,
            (unsigned long long)st.decompressed, (unsigned long long)st.raw_fallbacks,
-           (unsigned long long)st.pending_hits);
+           (unsigned long long)st.pending_hits, (unsigned long long)st.put_calls, (unsigned long long)st.get_calls,
+           st.t_iter, st.t_codec, st.t_put, st.t_get);
     fflush(stdout);
     return 0;
 }
@@ -397,14 +408,34 @@ void Server::apply(Req &q, std::string_view payload) {
 }
 
 void Server::process() {
-    if (codec == Codec::kBatch) run_codec();
+    if (codec != Codec::kBatch) return;
+    const double t0 = now_s();
+    run_codec();
+    st.t_codec += now_s() - t0;
 }
 
-// the iteration's codec work: one put batch and one get batch per GPU, GPUs on their own threads
+// the iteration's codec work: one put batch and one get batch per GPU; the put (compress stream)
+// and the get (decompress stream) of a GPU run side by side, and GPUs on their own threads
 void Server::run_codec() {
     auto work = [&](Gpu &g) {
         g.err = 0;
+        int gerr = 0;
         const uint32_t np = (uint32_t)g.puts.size(), ng = (uint32_t)g.gets.size();
+        std::thread getter;
+        if (ng) {
+            g.get_resp.assign(ng, nullptr);
+            g.get_len.assign(ng, 0);
+            g.get_rc.assign(ng, 0);
+            getter = std::thread([&] {
+                const double t0 = now_s();
+                gerr = pmc_store_get_batch(g.store, g.gets.data(), ng, PMC_FRAME_CUSTOM, g.get_resp.data(),
+                                           g.get_len.data(), g.get_rc.data());
+                if (&g == &gpus[0]) {
+                    st.t_get += now_s() - t0;
+                    st.get_calls++;
+                }
+            });
+        }
         if (np) {
             std::string blob;
             std::vector<uint64_t> off(np);
@@ -416,17 +447,16 @@ void Server::run_codec() {
             }
             g.put_ext.assign(np, pmc_extent{});
             g.put_rc.assign(np, 0);
+            const double t0 = now_s();
             g.err = pmc_store_put_batch(g.store, (const uint8_t *)blob.data(), off.data(), len.data(), np,
                                         g.put_ext.data(), g.put_rc.data());
+            if (&g == &gpus[0]) {
+                st.t_put += now_s() - t0;
+                st.put_calls++;
+            }
         }
-        if (ng) {
-            g.get_resp.assign(ng, nullptr);
-            g.get_len.assign(ng, 0);
-            g.get_rc.assign(ng, 0);
-            const int r = pmc_store_get_batch(g.store, g.gets.data(), ng, PMC_FRAME_CUSTOM, g.get_resp.data(),
-                                              g.get_len.data(), g.get_rc.data());
-            if (r) g.err = r;
-        }
+        if (getter.joinable()) getter.join();
+        if (gerr) g.err = gerr;
     };
     if (gpus.size() == 1) {
         work(gpus[0]);

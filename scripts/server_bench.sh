@@ -22,7 +22,8 @@ run off 4096 400000 16 50 &&
 run batch 4096 400000 16 50 &&
 run batch 4096 400000 64 50 &&
 run batch 4096 400000 64 0 &&
+run batch 4096 400000 256 50 &&
 run batch 4096 400000 64 100 &&
 run batch 1024 400000 64 50 &&
-run single 4096 20000 16 50 &&
-run single 1024 20000 16 50
+run single 4096 10000 16 50 &&
+run single 1024 10000 16 50

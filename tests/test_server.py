@@ -116,4 +116,4 @@ def test_server_on_gpu_codec(golden, codec):
     assert st["compressed"] > 8192 and st["decompressed"] > 0 and st["raw_fallbacks"] == 0, st
     if codec == "batch":
         assert st["pending_hits"] >= 1
-    print(codec, res)
+    print(codec, res, st)
