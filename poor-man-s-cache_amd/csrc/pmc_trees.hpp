@@ -8,8 +8,8 @@
 // symbols gets the longer code is decided by heap positions, so any other Huffman
 // construction would change output bytes.
 //
-// Written as __host__ __device__ so tests/test_trees_host.py can compile it with g++ and
-// diff it against oracle/trees.c on the CPU; on the GPU one lane of the wave runs it on
+// Written as __host__ __device__ so tests/host/host_pipeline.cpp (tests/test_host_pipeline.py) compiles it
+// with g++ and diffs it against oracle/trees.c on the CPU; on the GPU one lane of the wave runs it on
 // the wave's LDS-resident PmcTrees.
 #pragma once
 #include <stdint.h>
