@@ -919,6 +919,30 @@ struct SmallWave {
         const uint32_t l = (uint32_t)lane_id();
         if (l < (t.n & 63)) tok[(t.n & ~63u) + l] = t.v;
     }
+    // Implied literals: tokens cover the positions in order, so the literals between two matches
+    // are the run [lf, s) up to the next match's start s.  The parse only tracks lf; each match
+    // stores its run and itself with lane-parallel stores (lane k: token n + k), and the tail run
+    // [lf, len) goes out at the end -- no per-literal bookkeeping on the scalar unit.
+    __device__ void tb_match(TokBuf &t, uint32_t lf, uint32_t s, uint32_t m) {
+        const uint32_t l = (uint32_t)lane_id(), nl = s - lf, cnt = nl + 1;
+#ifndef PMC_DIAG_NOTOK
+        for (uint32_t b = 0; b < cnt; b += 64) {
+            const uint32_t k = b + l;
+            if (k < cnt) tok[t.n + k] = k < nl ? lf + k : m;
+        }
+#endif
+        t.n += cnt;
+    }
+    __device__ void tb_lits(TokBuf &t, uint32_t lf, uint32_t e) {
+        const uint32_t l = (uint32_t)lane_id(), cnt = e - lf;
+#ifndef PMC_DIAG_NOTOK
+        for (uint32_t b = 0; b < cnt; b += 64) {
+            const uint32_t k = b + l;
+            if (k < cnt) tok[t.n + k] = lf + k;
+        }
+#endif
+        t.n += cnt;
+    }
     // longest_match record of has-candidate position x (evaluating a new window if needed)
     template <bool PK>
     __device__ uint32_t group_get(Group &g, uint32_t x, uint32_t npos, uint32_t len) {
@@ -954,7 +978,7 @@ struct SmallWave {
         g.m = g.stop = g.fast = g.impr = g.cut = 0;
         g.e = 0;
         TokBuf tb;
-        uint32_t i = 0, ml = 2, ms = 0, av = 0;
+        uint32_t i = 0, ml = 2, ms = 0, lf = 0; // lf: first position of the pending literal run
         uint32_t hci = 0;              // HC word cached in SGPRs
 #if defined(PMC_DIAG_SALU) || defined(PMC_DIAG_VALU)
         uint32_t diag_s = 0, diag_s1 = 1, diag_s2 = 2, diag_s3 = 3, diag_v = 0, diag_v1 = 1, diag_v2 = 2, diag_v3 = 3;
@@ -965,7 +989,7 @@ struct SmallWave {
             i = rfl(i);
             ml = rfl(ml);
             ms = rfl(ms);
-            av = rfl(av);
+            lf = rfl(lf);
             tb.n = rfl(tb.n);
             count(14);
 #ifdef PMC_DIAG_SALU // diagnostic builds only: extra scalar / vector work per parse step
@@ -1007,10 +1031,7 @@ struct SmallWave {
                     }
                     if (m) j = w * 64 + (uint32_t)__builtin_ctzll(m);
                 }
-                if (j > i) {
-                    const uint32_t from = av ? i - 1 : i;
-                    tb_run(tb, from, j - 1 - from);
-                    av = 1;
+                if (j > i) { // (literals up to j stay implied)
                     i = j;
                     if (i >= len) break;
                 }
@@ -1030,18 +1051,11 @@ struct SmallWave {
                 }
                 const uint64_t sm = g.stop >> off;
                 if (!sm) { // literals to the window's end
-                    const uint32_t to = g.p0 + 64 < len ? g.p0 + 64 : len;
-                    const uint32_t from = av ? i - 1 : i;
-                    tb_run(tb, from, to - 1 - from);
-                    av = 1;
-                    i = to;
+                    i = g.p0 + 64 < len ? g.p0 + 64 : len;
                     continue;
                 }
                 const uint32_t sj = off + (uint32_t)__builtin_ctzll(sm), js = g.p0 + sj;
                 if (js > i) {
-                    const uint32_t from = av ? i - 1 : i;
-                    tb_run(tb, from, js - 1 - from);
-                    av = 1;
                     i = js;
                     if (!((g.m >> sj) & 1)) continue; // unevaluated: new window at js
                 }
@@ -1051,12 +1065,10 @@ struct SmallWave {
                     const uint32_t st = sj + (uint32_t)__builtin_ctzll(~(g.impr >> sj)), t = g.p0 + st;
                     const uint32_t e0 = readlane(g.e, (int)st);
                     const uint32_t b0 = e0 & 511, q0 = (e0 >> 9) & 0x3fffu;
-                    if (av) tb_put(tb, i - 1);
-                    tb_run(tb, i, t - i);
                     if ((g.fast >> st) & 1) {
-                        tb_put(tb, ((t - q0) << 16) | (b0 - 3));
+                        tb_match(tb, lf, t, ((t - q0) << 16) | (b0 - 3));
                         i = t + b0;
-                        av = 0;
+                        lf = i;
                         continue;
                     }
                     // whether t + 1 improves is not known here (cut or unevaluated): the general
@@ -1064,7 +1076,6 @@ struct SmallWave {
                     i = t + 1;
                     ml = b0;
                     ms = q0;
-                    av = 1;
                     continue;
                 }
             }
@@ -1095,22 +1106,19 @@ struct SmallWave {
                 }
             }
             if (pl >= 3 && ml <= pl) {
-                tb_put(tb, ((i - 1 - pm) << 16) | (pl - 3));
+                tb_match(tb, lf, i - 1, ((i - 1 - pm) << 16) | (pl - 3));
                 i += pl - 1;
+                lf = i;
                 ml = 2;
-                av = 0;
             } else {
-                if (av) tb_put(tb, i - 1);
-                av = 1;
                 i++;
             }
         }
-        if (av) tb_put(tb, i - 1);
+        tb_lits(tb, lf, len);
 #if defined(PMC_DIAG_SALU) || defined(PMC_DIAG_VALU)
         if (rfl(diag_s + diag_s1 + diag_s2 + diag_s3 + diag_v + diag_v1 + diag_v2 + diag_v3) == 0xdeadbeefu)
-            tb_put(tb, 0); // (keeps the diagnostic work alive)
+            tb_lits(tb, 0, 1); // (keeps the diagnostic work alive)
 #endif
-        tb_finish(tb);
         wave_sync_global();
         return rfl(tb.n);
     }
