@@ -279,6 +279,15 @@ struct TreeOut {
 #ifndef PMC_PRECAND
 #define PMC_PRECAND 32
 #endif
+// A uniform 0/1 integer the compiler may not turn back into a bool: branching on it is one
+// s_cmp + s_cbranch_scc.  (Bools merged across blocks become 64-bit lane masks -- s_cselect_b64,
+// s_and_b64 with exec, s_cbranch_vcc -- on the scalar unit, which the parse saturates.)
+__device__ __forceinline__ uint32_t sflag(uint32_t x) {
+    x = __builtin_amdgcn_readfirstlane(x);
+    asm volatile("" : "+s"(x));
+    return x;
+}
+
 struct SmallWave {
     // every working array is LDS-typed (ds_* with 32-bit addresses)
     PMC_LDS uint8_t *b;
@@ -1031,10 +1040,11 @@ struct SmallWave {
                     }
                     if (m) j = w * 64 + (uint32_t)__builtin_ctzll(m);
                 }
-                if (j > i) { // (literals up to j stay implied)
-                    i = j;
-                    if (i >= len) break;
-                }
+                // (j >= i; literals up to j stay implied.  Unconditional updates and single integer
+                // tests keep each branch one s_cmp: bool values merged across blocks became lane-mask
+                // selects on the scalar unit this kernel saturates)
+                i = j;
+                if (i >= len) break;
                 // Window walk from a fresh state at has-candidate position i (< npos): in the
                 // evaluated window, unusable results pass as literals and a usable one that
                 // position + 1 does not improve on is emitted at once (eval_group's stop / fast
@@ -1042,7 +1052,8 @@ struct SmallWave {
                 // improvements take the general step below; an unevaluated position with
                 // candidates starts a new window.
                 uint32_t off = i - g.p0;
-                if (!(off < 64 && ((g.m >> off) & 1))) {
+                const uint32_t inwin = sflag((uint32_t)(g.m >> (off & 63)) & (off < 64 ? 1u : 0u));
+                if (!inwin) {
                     stamp(2);
                     eval_group<PK>(g, i, npos, len);
                     stamp(10);
@@ -1055,17 +1066,15 @@ struct SmallWave {
                     continue;
                 }
                 const uint32_t sj = off + (uint32_t)__builtin_ctzll(sm), js = g.p0 + sj;
-                if (js > i) {
-                    i = js;
-                    if (!((g.m >> sj) & 1)) continue; // unevaluated: new window at js
-                }
-                if (!((g.cut >> sj) & 1)) {
+                i = js;                               // (js >= i)
+                if (!sflag((uint32_t)(g.m >> sj) & 1u)) continue; // unevaluated: new window at js
+                if (!sflag((uint32_t)(g.cut >> sj) & 1u)) {
                     // usable at js: the run of lazy improvements js, js + 1, ... ends at t (bit
                     // 63 of impr is always clear); positions js .. t - 1 become literals
                     const uint32_t st = sj + (uint32_t)__builtin_ctzll(~(g.impr >> sj)), t = g.p0 + st;
                     const uint32_t e0 = readlane(g.e, (int)st);
                     const uint32_t b0 = e0 & 511, q0 = (e0 >> 9) & 0x3fffu;
-                    if ((g.fast >> st) & 1) {
+                    if (sflag((uint32_t)(g.fast >> st) & 1u)) {
                         tb_match(tb, lf, t, ((t - q0) << 16) | (b0 - 3));
                         i = t + b0;
                         lf = i;
@@ -1082,12 +1091,12 @@ struct SmallWave {
             count(9);
             const uint32_t pl = ml, pm = ms;
             ml = 2;
-            if (i < npos && pl < 258) {
+            if (sflag((i < npos ? 1u : 0u) & (pl < 258 ? 1u : 0u))) {
                 if ((i >> 6) != hci) {
                     hci = i >> 6;
                     hcw = rfl64(HC[hci]);
                 }
-                if ((hcw >> (i & 63)) & 1) {
+                if (sflag((uint32_t)(hcw >> (i & 63)) & 1u)) {
                     const uint32_t e = group_get<PK>(g, i, npos, len);
                     uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
                     if (e >> 31) {
@@ -1105,7 +1114,7 @@ struct SmallWave {
                     }
                 }
             }
-            if (pl >= 3 && ml <= pl) {
+            if (sflag((pl >= 3 ? 1u : 0u) & (ml <= pl ? 1u : 0u))) {
                 tb_match(tb, lf, i - 1, ((i - 1 - pm) << 16) | (pl - 3));
                 i += pl - 1;
                 lf = i;
