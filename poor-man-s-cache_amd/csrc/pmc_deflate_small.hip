@@ -101,11 +101,18 @@ __host__ __device__ inline SmallLayout small_layout(uint64_t n) {
     return L;
 }
 uint64_t deflate_small_wave_bytes(uint64_t n) { return small_layout(n).total; }
+// Chain counts packed into the top bits of R (ranks use ceil(log2 n) bits): 6 bits for n <= 1024,
+// 4 bits for 3072 < n <= 4096 (0 = not packed: a separate u8 CN array).  A count field holds the exact
+// count below its maximum; the maximum means "at least that many".  4 bits saturate below the eval's
+// 32 lanes per position (more cut walks), which pays only where dropping the n-byte CN array buys a
+// wave per SIMD: same-box A/B, 4 KiB front 256 -> 244 ms (7 waves/CU instead of 6); at 2 KiB, 5 bits
+// made the front 4 % slower.
+__host__ __device__ inline int front_pkb(uint64_t n) { return n <= 1024 ? 6 : (n > 3072 && n <= 4096) ? 4 : 0; }
 // split-pipeline front: bytes | S | R | X (sort table, then the parse's HC bits); the symbol
 // histograms overlay S and R after the parse
 struct FrontLayout {
     uint64_t bytes, S, R, X, freq, total;
-    bool pk;             // chain counts packed into R's top 6 bits (n <= 1024: R < 1024)
+    int pkb;             // chain-count bits packed into R's top (front_pkb), 0: CN array
     uint64_t cn, hc, ev; // parse scratch in X (cn unused when pk); the sort's 512-B table at X
 };
 __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
@@ -115,9 +122,9 @@ __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
     F.S = a(n + 32);
     F.R = F.S + a(2 * n + 2);
     F.X = F.R + a(2 * n + 2);
-    F.pk = n <= 1024;
+    F.pkb = front_pkb(n);
     F.cn = F.X;
-    F.hc = F.pk ? F.X : F.X + a(n);
+    F.hc = F.pkb ? F.X : F.X + a(n);
     F.ev = F.hc + a(((n + 63) / 64) * 8);
     const uint64_t xe = F.ev + 320 > F.X + 512 ? F.ev + 320 : F.X + 512;
     F.freq = F.S;
@@ -306,7 +313,7 @@ struct SmallWave {
     PMC_LDS uint64_t *HC;   // on-demand parse: bit x = position x has a chain candidate (aliases M)
     PMC_LDS uint8_t *CN;    // on-demand parse: chain candidates of position x (capped at 255)
     PMC_LDS uint32_t *EV;   // on-demand parse: eval scratch (64 best keys, 64 u8 owner marks)
-    bool cnp;               // chain counts live in R's top 6 bits (values <= 1024 bytes), CN unused
+    int cnp;                // chain-count bits in R's top (front_pkb: 6 / 5 / 4), 0: counts in CN
     PMC_LDS uint64_t *ML;   // segment walk: positions that start a match (or are unresolved)
     PMC_LDS uint64_t *MP;   // segment walk: positions where a lazy-improvement run ends
     PMC_GLB uint32_t *tok;
@@ -563,7 +570,7 @@ struct SmallWave {
     // Resumes a walk cut short by match_all: candidates kPreCand.. of position i, starting
     // from that walk's best / bestq.  Returns the match length (> b0) or 0; *q_out = the
     // nearest candidate achieving it.
-    template <bool PK>
+    template <int PK>
     __device__ __forceinline__ uint32_t search(uint32_t i, uint32_t b0, uint32_t len, uint32_t best, uint32_t bestq,
                                uint32_t *q_out) {
         const int l = lane_id();
@@ -571,7 +578,7 @@ struct SmallWave {
         const uint32_t nice = (len - i) < 258 ? (len - i) : 258;
         const uint32_t wi = load4(i);
         const uint32_t hi = hash3(wi);
-        const int r = (int)(PK ? R[i] & 1023u : (uint32_t)R[i]);
+        const int r = (int)(PK ? R[i] & ((1u << (16 - PK)) - 1u) : (uint32_t)R[i]);
         uint32_t examined = kPreCand;
         for (int kb = r - 1 - (int)kPreCand;; kb -= 64) {
             const uint32_t thr = best > b0 ? best : b0;
@@ -741,8 +748,9 @@ struct SmallWave {
     // CN[x] = chain candidates of x = entries before x in its run of the hash-sorted order,
     // less position 0 (zlib's NIL: head[] value 0 never starts a match; the sort is stable,
     // so position 0 is the first entry of its run).  HC = CN > 0 as bits.
-    template <bool PK>
+    template <int PK>
     __device__ __forceinline__ void build_cn(uint32_t npos) {
+        constexpr uint32_t RB = 16 - PK, CMAX = PK ? (1u << PK) - 1 : 255u;
         const uint32_t l = (uint32_t)lane_id();
         const uint32_t k0 = rfl((uint32_t)R[0]);
         uint32_t ph = 0xffffffffu, prs = 0; // previous chunk's last hash and run start
@@ -757,7 +765,7 @@ struct SmallWave {
             rs = rs > prs ? rs : prs;
             const uint32_t cnt = k - rs - (rs == k0 && k > rs ? 1u : 0u);
             if (valid) {
-                if (PK) R[p] = (uint16_t)(k | (cnt < 63 ? cnt : 63) << 10);
+                if (PK) R[p] = (uint16_t)(k | (cnt < CMAX ? cnt : CMAX) << RB);
                 else CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
             }
             ph = readlane(h, 63);
@@ -766,7 +774,7 @@ struct SmallWave {
         wave_sync();
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
             const uint32_t x = c0 + l;
-            const uint64_t m = ballot(x < npos && (PK ? (R[x] >> 10) : (uint32_t)CN[x]) != 0);
+            const uint64_t m = ballot(x < npos && (PK ? ((uint32_t)R[x] >> RB) : (uint32_t)CN[x]) != 0);
             if (l == 0) HC[c0 >> 6] = m;
         }
         wave_sync();
@@ -796,23 +804,28 @@ struct SmallWave {
     // (4) 16 bytes at the candidate; then 16 bytes per step while some lane still matches;
     // (5) an LDS max per position and its read-back.  Lanes outside the evaluated prefix
     // compute on clamped indices and contribute key 0 (no exec-mask branches).
-    template <bool PK>
+    template <int PK>
     __device__ void eval_group(Group &g, uint32_t p0, uint32_t npos, uint32_t len) {
+        // SAT: a count field narrower than kPreCand saturates below it; such a position gets
+        // kPreCand lanes whose candidates are validated (same hash, inside the array, not NIL) and
+        // is marked cut (search() resumes it exactly if the parse needs it)
+        constexpr uint32_t RB = 16 - PK, CMAX = PK ? (1u << PK) - 1 : 255u;
+        constexpr bool SAT = CMAX < kPreCand;
         const uint32_t l = (uint32_t)lane_id();
         const uint32_t x = p0 + l;
         const uint32_t xc = x < npos ? x : 0u, x1 = x + 1 < npos ? x + 1 : 0u;
         uint32_t rx = R[xc], cn, cn1;
         if (PK) {
-            cn = rx >> 10;
-            rx &= 1023u;
-            cn1 = (uint32_t)R[x1] >> 10;
+            cn = rx >> RB;
+            rx &= (1u << RB) - 1u;
+            cn1 = (uint32_t)R[x1] >> RB;
         } else {
             cn = CN[xc];
             cn1 = CN[x1];
         }
         cn = x < npos ? cn : 0u;
         cn1 = x + 1 < npos ? cn1 : 0u;
-        const uint32_t w = cn < kPreCand ? cn : kPreCand;
+        const uint32_t w = SAT && cn == CMAX ? kPreCand : cn < kPreCand ? cn : kPreCand;
         const uint32_t incl = wave_incl_scan_dpp(w), offs = incl - w;
         const bool inc = w != 0 && incl <= 64;
         const uint64_t im = ballot(inc); // a prefix of the window's has-candidate offsets
@@ -829,11 +842,14 @@ struct SmallWave {
         const uint32_t sc = wave_incl_max_dpp(mk);
         const uint32_t own = v ? ((sc >> 19) & 127) - 1 : 0u;
         const uint32_t P = p0 + own, d = l - (sc >> 26) + 1;
-        uint32_t q = S[v ? (sc & 0x7ffffu) - d : 0u];
+        const uint32_t rxo = sc & 0x7ffffu;
+        uint32_t q = S[v && (!SAT || rxo >= d) ? rxo - d : 0u];
         uint64_t A0, A1, B0, B1;
         load16(P, A0, A1);
         q = v ? q : 0u;
         load16(q, B0, B1);
+        // (SAT) lanes past the chain: another hash, below the array, or position 0 (NIL)
+        const bool vk = v && (!SAT || (rxo >= d && q != 0u && hash3((uint32_t)A0) == hash3((uint32_t)B0)));
         const uint32_t nice = (len - P) < 258 ? (len - P) : 258;
         // (branch-free on the vector ALU: 0/1 integers and products instead of bools and
         // selects, which became exec-mask and lane-mask work on the saturated scalar unit)
@@ -861,13 +877,13 @@ struct SmallWave {
             off += 16;
         }
         cl = cl < nice ? cl : nice;
-        __hip_atomic_fetch_max(&EV[own], v ? cl << 23 | (kPreCand - d) << 18 | q : 0u, __ATOMIC_RELAXED,
+        __hip_atomic_fetch_max(&EV[own], vk ? cl << 23 | (kPreCand - d) << 18 | q : 0u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WAVEFRONT);
         wave_sync();
         const uint32_t kk = EV[l], best = kk >> 23;
         const uint32_t nx = (len - x) < 258 ? (len - x) : 258;
         auto neg = [](uint32_t d) { return d >> 31; }; // 1 iff d < 0 as int (all values here are small)
-        uint32_t cutc = neg(kPreCand - cn) & neg(best - nx);
+        uint32_t cutc = (SAT ? (cn == CMAX ? 1u : 0u) : neg(kPreCand - cn)) & neg(best - nx);
         const uint32_t bq = kk & 0x3fffu, e = best | bq << 9 | cutc << 31;
         g.p0 = p0;
         g.m = im;
@@ -953,7 +969,7 @@ struct SmallWave {
         t.n += cnt;
     }
     // longest_match record of has-candidate position x (evaluating a new window if needed)
-    template <bool PK>
+    template <int PK>
     __device__ uint32_t group_get(Group &g, uint32_t x, uint32_t npos, uint32_t len) {
         const uint32_t off = x - g.p0;
         if (off < 64 && ((g.m >> off) & 1)) return readlane(g.e, (int)off);
@@ -965,7 +981,7 @@ struct SmallWave {
     }
     // (a noinline member reaches the wave state through `this`, a pointer to scratch: every
     // member pointer would be re-read from memory inside the loop.  A local copy lives in SGPRs.)
-    template <bool PK>
+    template <int PK>
     __device__ __noinline__ uint32_t parse_ondemand(uint32_t npos_, uint32_t len_) {
         SmallWave me = *this;
         const uint32_t r = me.parse_ondemand_body<PK>(npos_, len_);
@@ -975,7 +991,7 @@ struct SmallWave {
 #endif
         return r;
     }
-    template <bool PK>
+    template <int PK>
     __device__ __forceinline__ uint32_t parse_ondemand_body(uint32_t npos_, uint32_t len_) {
         const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
         const uint32_t nw = (npos + 63) >> 6;
@@ -1870,7 +1886,9 @@ struct SmallWave {
             sort_positions2(npos, (PMC_LDS uint32_t *)CN);
             stamp(1);
             PMC_STOP(12, 0)
-            ntok = cnp ? parse_ondemand<true>(npos, len) : parse_ondemand<false>(npos, len);
+            ntok = cnp == 6   ? parse_ondemand<6>(npos, len)
+                   : cnp == 4 ? parse_ondemand<4>(npos, len)
+                              : parse_ondemand<0>(npos, len);
             PMC_STOP(14, 0)
         } else {
             lit_run(0, 0, len);
@@ -2021,7 +2039,7 @@ __device__ inline void small_wave_init(SmallWave &w, uint8_t *base, const SmallL
     w.cnt = to_lds<uint16_t>(base + L.cnt);
     w.M = to_lds<uint32_t>(base + L.M);
     w.CN = to_lds<uint8_t>(base + L.M);
-    w.cnp = false;
+    w.cnp = 0;
     w.HC = to_lds<uint64_t>(base + L.M + cn_hc_offset(a.cap_len));
     w.EV = to_lds<uint32_t>(base + L.M + cn_ev_offset(a.cap_len));
     w.crc_tab = to_lds<const uint32_t>((void *)crc_tab);
@@ -2071,7 +2089,7 @@ __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
     w.cnt = to_lds<uint16_t>(base + L.cnt);
     w.M = to_lds<uint32_t>(base + L.M);
     w.CN = to_lds<uint8_t>(base + L.M);
-    w.cnp = false;
+    w.cnp = 0;
     w.HC = to_lds<uint64_t>(base + L.M + cn_hc_offset(a.cap_len));
     w.EV = to_lds<uint32_t>(base + L.M + cn_ev_offset(a.cap_len));
     w.ML = to_lds<uint64_t>(base + L.masks);

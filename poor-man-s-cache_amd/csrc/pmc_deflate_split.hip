@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     w.CN = to_lds<uint8_t>(base + F.cn);
     w.HC = to_lds<uint64_t>(base + F.hc);
     w.EV = to_lds<uint32_t>(base + F.ev);
-    w.cnp = F.pk;
+    w.cnp = F.pkb;
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;
