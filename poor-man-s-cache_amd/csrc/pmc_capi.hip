@@ -267,6 +267,21 @@ uint64_t deflate_small_limit() {
 }
 
 // `extra` = dynamic LDS per block besides the waves' working sets (the CRC table; 0 for the front).
+// values up to this length take the split pipeline's large pass: the front's working set (no chain
+// counts) and the back's must fit a CU's LDS, and every match distance must stay <= MAX_DIST
+// (32506; longer values would need zlib's window limit in the candidate walk)
+uint64_t deflate_big_limit() {
+    uint64_t lo = kSmallMax, hi = 32506;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi + 1) / 2;
+        if (deflate_front_wave_bytes(mid) <= kLdsPerCu && deflate_back_wave_bytes(mid) + kCrcTabBytes <= kLdsPerCu)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
 Launch plan_lds(pmc_ctx *ctx, const void *kernel, uint64_t wave_bytes, uint64_t n_items,
                 uint64_t extra = kCrcTabBytes) {
     Launch L;
@@ -408,45 +423,51 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     DeflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, nullptr,
                   ctx->dbg, -1};
     if (const char *e = getenv("PMC_STOP_AFTER")) a.stop_after = atoi(e); // diagnostic builds only
-    // Values <= small_lim: single-block LDS kernel (pmc_deflate_small.hip).  Larger values:
-    // the general kernel with its working set in HBM (pmc_deflate.hip).  PMC_DEFLATE_V1=1
-    // routes everything through the general kernels (A/B and safety net).
+    // Values <= small_lim (16382): the split pipeline's small pass; 16382 < len <= big_lim (~31.9K,
+    // the front's 160 KiB LDS; MAX_DIST caps it at 32506): its large pass; the rest -- and
+    // large-pass values of >= 16383 symbols, which need several DEFLATE blocks -- the general
+    // kernel with its working set in HBM (pmc_deflate.hip).  PMC_DEFLATE_V1=1 routes everything
+    // through the general kernels (A/B and safety net); PMC_DEFLATE_MONO=1 the single-kernel path.
     static const bool force_v1 = getenv("PMC_DEFLATE_V1") && atoi(getenv("PMC_DEFLATE_V1"));
+    static const bool mono = getenv("PMC_DEFLATE_MONO") && atoi(getenv("PMC_DEFLATE_MONO"));
+    static const bool no_big = getenv("PMC_BIG_PASS") && !atoi(getenv("PMC_BIG_PASS"));
+    const bool split = !force_v1 && !mono;
     const uint64_t small_lim = force_v1 ? 0 : deflate_small_limit();
+    const uint64_t big_lim = split && !no_big ? deflate_big_limit() : small_lim;
     const uint64_t v1_lim = deflate_lds_limit();
     const uint64_t lds_cut = force_v1 ? std::min<uint64_t>(v1_lim, std::max<uint64_t>(max_len, 1))
                                       : std::min<uint64_t>(small_lim, std::max<uint64_t>(max_len, 1));
     uint64_t cap = (lds_cut + 63) & ~(uint64_t)63;
     cap = std::min<uint64_t>(cap, force_v1 ? v1_lim : small_lim);
+    // large pass: values in (small_lim, big_hi]
+    const bool big_pass = split && max_len > small_lim && big_lim > small_lim;
+    const uint64_t big_hi = big_pass ? std::min<uint64_t>(big_lim, max_len) : 0;
+    const uint64_t big_cap = big_pass ? std::min<uint64_t>((big_hi + 63) & ~(uint64_t)63, big_lim) : 0;
+    const uint64_t hbm_cut = big_pass ? big_hi : lds_cut; // the HBM kernel takes lengths above this
     uint64_t hbm_waves = 0, hbm_wb = 0;
-    if (max_len > lds_cut) {
+    if (max_len > hbm_cut || big_pass) {
         hbm_wb = deflate_wave_bytes(true, max_len);
         hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 2,
                                                              (8ull << 30) / std::max<uint64_t>(hbm_wb, 1)));
         hbm_waves = std::min<uint64_t>(hbm_waves, n);
     }
-    // Small values: the split pipeline (pmc_deflate_split.hip: front -> lane-parallel trees ->
-    // back, chunk by chunk) unless PMC_DEFLATE_MONO=1 selects the single-kernel path.
-    static const bool mono = getenv("PMC_DEFLATE_MONO") && atoi(getenv("PMC_DEFLATE_MONO"));
-    if (!force_v1 && !mono) {
-        const uint64_t fwb = deflate_front_wave_bytes(cap), bwb = deflate_back_wave_bytes(cap);
-        // the front keeps no CRC table in LDS: its grid is sized for the blocks that really fit
-        // (PMC_FRONT_PLAN_CRC=1: the former plan, which reserved 1 KiB per block for it)
-        static const bool front_crc = getenv("PMC_FRONT_PLAN_CRC") && atoi(getenv("PMC_FRONT_PLAN_CRC"));
-        Launch Lf = plan_lds(ctx, (const void *)deflate_front_kernel, fwb, n, front_crc ? kCrcTabBytes : 0);
-        const size_t front_lds = Lf.lds - (front_crc ? kCrcTabBytes : 0);
-        Launch Lb = plan_lds(ctx, (const void *)deflate_back_kernel, bwb, n);
+    if (split) {
         // chunk scratch budget (PMC_SPLIT_CHUNK_MB): 16 GiB of the 288 GiB holds 2.2M 1-KiB values, 5 launches
         // per 10M; measured best against 2-12 GiB (fewer kernel tails)
         static const uint64_t budget = (getenv("PMC_SPLIT_CHUNK_MB") ? (uint64_t)atoll(getenv("PMC_SPLIT_CHUNK_MB"))
                                                                      : 16384ull) << 20;
-        const uint64_t per = split_value_bytes(cap);
-        uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(4096, budget / per));
-        chunk = (chunk + 63) & ~(uint64_t)63;
-        const uint64_t blocks = chunk / 64;
-        int r = ctx->split.ensure(chunk * cap * 4 + chunk * 4 + chunk * 4 + blocks * 64 * kSplitRows * 3 +
-                                  blocks * 64 * kMergeRows * 4 + (chunk + 1) * 4 + chunk * 8 +
-                                  kOrderBins * 4 + 64 + 1024);
+        auto chunk_of = [&](uint64_t c) {
+            uint64_t ch = std::min<uint64_t>(n, std::max<uint64_t>(4096, budget / split_value_bytes(c)));
+            return (ch + 63) & ~(uint64_t)63;
+        };
+        auto scratch_of = [&](uint64_t c, uint64_t ch) {
+            const uint64_t blocks = ch / 64;
+            return ch * c * 4 + ch * 4 + ch * 4 + blocks * 64 * kSplitRows * 3 + blocks * 64 * kMergeRows * 4 +
+                   (ch + 1) * 4 + ch * 8 + kOrderBins * 4 + 64 + 1024;
+        };
+        uint64_t need = scratch_of(cap, chunk_of(cap));
+        if (big_pass) need = std::max<uint64_t>(need, scratch_of(big_cap, chunk_of(big_cap)));
+        int r = ctx->split.ensure(need);
         if (r) return r;
         if (hbm_waves) {
             r = ctx->tokens.ensure(hbm_waves * kSlabSyms * sizeof(uint32_t));
@@ -454,71 +475,88 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
             r = ctx->dscratch.ensure(hbm_waves * hbm_wb);
             if (r) return r;
         }
-        uint8_t *p = (uint8_t *)ctx->split.p;
-        a.cT = (uint32_t *)p;
-        p += chunk * cap * 4;
-        a.cN = (uint32_t *)p;
-        p += chunk * 4;
-        a.cP = (uint32_t *)p;
-        p += chunk * 4;
-        a.cG = (uint32_t *)p;
-        p += blocks * 64 * kMergeRows * 4;
-        a.cH = (uint16_t *)p;
-        p += blocks * 64 * kSplitRows * 2;
-        a.cL = (uint8_t *)p;
-        p += blocks * 64 * kSplitRows;
-        a.cD = (uint32_t *)p;
-        p += (chunk + 1) * 4;
-        a.cZ = (uint32_t *)p;
-        p += chunk * 4;
-        uint32_t *ord = (uint32_t *)p;
-        p += chunk * 4;
-        uint32_t *obins = (uint32_t *)p;
-        p += kOrderBins * 4;
-        a.cQ = (uint32_t *)p;
         static const bool no_order = getenv("PMC_TREES_ORDER") && !atoi(getenv("PMC_TREES_ORDER"));
-        a.lds_max_len = lds_cut;
-        a.cap_len = cap;
+        // the front keeps no CRC table in LDS: its grid is sized for the blocks that really fit
+        // (PMC_FRONT_PLAN_CRC=1: the former plan, which reserved 1 KiB per block for it)
+        static const bool front_crc = getenv("PMC_FRONT_PLAN_CRC") && atoi(getenv("PMC_FRONT_PLAN_CRC"));
         const size_t tl_small = (size_t)(kTreesCap + 1) * 64 * 4 + 36 * 64 * 2;
         const size_t tl_big = (size_t)(kLCodes + 1) * 64 * 4 + 36 * 64 * 2;
-        for (uint64_t first = 0; first < n; first += chunk) {
-            a.first = first;
-            a.count = std::min<uint64_t>(chunk, n - first);
-            const unsigned tb = (unsigned)((a.count + 63) / 64);
-            a.wave_bytes = fwb;
-            if (hipMemsetAsync(a.cQ, 0, 8, st) != hipSuccess) return PMC_E_NO_DEVICE;
-            klaunch(ctx, PMC_K_DEFLATE_FRONT, st, [&] {
-                hipLaunchKernelGGL(deflate_front_kernel,
-                                   dim3((unsigned)std::min<uint64_t>(Lf.blocks, (a.count + Lf.wpb - 1) / Lf.wpb)),
-                                   dim3(64 * Lf.wpb), front_lds, st, a);
-            });
-            if (hipMemsetAsync(a.cD + a.count, 0, 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
-            // trees visit order by used literal/length symbols (PMC_TREES_ORDER=0: index order)
-            a.cO = nullptr;
-            if (!no_order && a.count >= 4096) {
-                if (hipMemsetAsync(obins, 0, kOrderBins * 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
-                const unsigned ob = (unsigned)std::min<uint64_t>((a.count + 1023) / 1024, (uint64_t)ctx->cus * 4);
-                klaunch(ctx, PMC_K_ORDER, st, [&] {
-                    hipLaunchKernelGGL(order_hist_kernel, dim3(ob), dim3(256), 0, st, (const uint32_t *)a.cZ, a.count,
-                                       obins);
-                    hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, st, obins);
-                    hipLaunchKernelGGL(order_scatter_kernel, dim3(ob), dim3(256), 0, st, (const uint32_t *)a.cZ,
-                                       a.count, obins, ord);
+        // one pass over the batch for the values with lo < len <= hi, working sets sized for pcap
+        auto run_pass = [&](uint64_t lo, uint64_t hi, uint64_t pcap) -> int {
+            const uint64_t fwb = deflate_front_wave_bytes(pcap), bwb = deflate_back_wave_bytes(pcap);
+            Launch Lf = plan_lds(ctx, (const void *)deflate_front_kernel, fwb, n, front_crc ? kCrcTabBytes : 0);
+            const size_t front_lds = Lf.lds - (front_crc ? kCrcTabBytes : 0);
+            Launch Lb = plan_lds(ctx, (const void *)deflate_back_kernel, bwb, n);
+            const uint64_t chunk = chunk_of(pcap), blocks = chunk / 64;
+            uint8_t *p = (uint8_t *)ctx->split.p;
+            a.cT = (uint32_t *)p;
+            p += chunk * pcap * 4;
+            a.cN = (uint32_t *)p;
+            p += chunk * 4;
+            a.cP = (uint32_t *)p;
+            p += chunk * 4;
+            a.cG = (uint32_t *)p;
+            p += blocks * 64 * kMergeRows * 4;
+            a.cH = (uint16_t *)p;
+            p += blocks * 64 * kSplitRows * 2;
+            a.cL = (uint8_t *)p;
+            p += blocks * 64 * kSplitRows;
+            a.cD = (uint32_t *)p;
+            p += (chunk + 1) * 4;
+            a.cZ = (uint32_t *)p;
+            p += chunk * 4;
+            uint32_t *ord = (uint32_t *)p;
+            p += chunk * 4;
+            uint32_t *obins = (uint32_t *)p;
+            p += kOrderBins * 4;
+            a.cQ = (uint32_t *)p;
+            a.min_len = lo;
+            a.lds_max_len = hi;
+            a.cap_len = pcap;
+            for (uint64_t first = 0; first < n; first += chunk) {
+                a.first = first;
+                a.count = std::min<uint64_t>(chunk, n - first);
+                const unsigned tb = (unsigned)((a.count + 63) / 64);
+                a.wave_bytes = fwb;
+                if (hipMemsetAsync(a.cQ, 0, 8, st) != hipSuccess) return PMC_E_NO_DEVICE;
+                klaunch(ctx, PMC_K_DEFLATE_FRONT, st, [&] {
+                    hipLaunchKernelGGL(deflate_front_kernel,
+                                       dim3((unsigned)std::min<uint64_t>(Lf.blocks, (a.count + Lf.wpb - 1) / Lf.wpb)),
+                                       dim3(64 * Lf.wpb), front_lds, st, a);
                 });
-                a.cO = ord;
+                if (hipMemsetAsync(a.cD + a.count, 0, 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
+                // trees visit order by used literal/length symbols (PMC_TREES_ORDER=0: index order)
+                a.cO = nullptr;
+                if (!no_order && a.count >= 4096) {
+                    if (hipMemsetAsync(obins, 0, kOrderBins * 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
+                    const unsigned ob = (unsigned)std::min<uint64_t>((a.count + 1023) / 1024, (uint64_t)ctx->cus * 4);
+                    klaunch(ctx, PMC_K_ORDER, st, [&] {
+                        hipLaunchKernelGGL(order_hist_kernel, dim3(ob), dim3(256), 0, st, (const uint32_t *)a.cZ,
+                                           a.count, obins);
+                        hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(1024), 0, st, obins);
+                        hipLaunchKernelGGL(order_scatter_kernel, dim3(ob), dim3(256), 0, st, (const uint32_t *)a.cZ,
+                                           a.count, obins, ord);
+                    });
+                    a.cO = ord;
+                }
+                klaunch(ctx, PMC_K_DEFLATE_TREES, st, [&] {
+                    hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap>, dim3(tb), dim3(64), tl_small, st, a);
+                    hipLaunchKernelGGL(deflate_trees_kernel<kLCodes>, dim3(std::min<unsigned>(tb, (unsigned)ctx->cus)),
+                                       dim3(64), tl_big, st, a);
+                });
+                a.wave_bytes = bwb;
+                klaunch(ctx, PMC_K_DEFLATE_BACK, st, [&] {
+                    hipLaunchKernelGGL(deflate_back_kernel,
+                                       dim3((unsigned)std::min<uint64_t>(Lb.blocks, (a.count + Lb.wpb - 1) / Lb.wpb)),
+                                       dim3(64 * Lb.wpb), Lb.lds, st, a);
+                });
             }
-            klaunch(ctx, PMC_K_DEFLATE_TREES, st, [&] {
-                hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap>, dim3(tb), dim3(64), tl_small, st, a);
-                hipLaunchKernelGGL(deflate_trees_kernel<kLCodes>, dim3(std::min<unsigned>(tb, (unsigned)ctx->cus)),
-                                   dim3(64), tl_big, st, a);
-            });
-            a.wave_bytes = bwb;
-            klaunch(ctx, PMC_K_DEFLATE_BACK, st, [&] {
-                hipLaunchKernelGGL(deflate_back_kernel,
-                                   dim3((unsigned)std::min<uint64_t>(Lb.blocks, (a.count + Lb.wpb - 1) / Lb.wpb)),
-                                   dim3(64 * Lb.wpb), Lb.lds, st, a);
-            });
-        }
+            return PMC_OK;
+        };
+        r = run_pass(0, lds_cut, cap);
+        if (!r && big_pass) r = run_pass(small_lim, big_hi, big_cap);
+        if (r) return r;
+        a.min_len = 0;
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
             set_err("deflate split pipeline", e);
@@ -557,6 +595,8 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     // ---- HBM kernel (values > lds_cut) ----
     if (hbm_waves) {
         a.cap_len = max_len;
+        a.lds_max_len = hbm_cut;
+        a.retry = big_pass ? 1 : 0;
         a.wave_bytes = hbm_wb;
         a.scratch = (uint8_t *)ctx->dscratch.p;
         klaunch(ctx, PMC_K_DEFLATE_HBM, st, [&] {

@@ -523,7 +523,9 @@ __global__ void __launch_bounds__(256) deflate_kernel(DeflateArgs a) {
       const uint64_t vl = g + (uint64_t)l;
       const uint64_t myl = vl < a.n ? a.src_len[vl] : 0;
       // values above cap_len (the call's max_len) are argument errors (arg_check_kernel)
-      uint64_t todo = ballot(vl < a.n && (kHbm ? (myl > a.lds_max_len && myl <= a.cap_len) : (myl <= a.lds_max_len)));
+      uint64_t todo = ballot(vl < a.n && (kHbm ? ((myl > a.lds_max_len && myl <= a.cap_len) ||
+                                                   (a.retry && a.rc[vl] == kDeflateRetry))
+                                                : (myl <= a.lds_max_len)));
       while (todo) {
         const uint64_t v = g + (uint64_t)__builtin_ctzll(todo);
         todo &= todo - 1;

@@ -107,12 +107,16 @@ uint64_t deflate_small_wave_bytes(uint64_t n) { return small_layout(n).total; }
 // 32 lanes per position (more cut walks), which pays only where dropping the n-byte CN array buys a
 // wave per SIMD: same-box A/B, 4 KiB front 256 -> 244 ms (7 waves/CU instead of 6); at 2 KiB, 5 bits
 // made the front 4 % slower.
-__host__ __device__ inline int front_pkb(uint64_t n) { return n <= 1024 ? 6 : (n > 3072 && n <= 4096) ? 4 : 0; }
+// Values above 16382 bytes (the large pass, up to deflate_big_limit()) keep no counts at all (-1):
+// the has-candidate bits HC stand in, every such position gets kPreCand validated lanes and is cut.
+__host__ __device__ inline int front_pkb(uint64_t n) {
+    return n <= 1024 ? 6 : (n > 3072 && n <= 4096) ? 4 : n > kSmallMax ? -1 : 0;
+}
 // split-pipeline front: bytes | S | R | X (sort table, then the parse's HC bits); the symbol
 // histograms overlay S and R after the parse
 struct FrontLayout {
     uint64_t bytes, S, R, X, freq, total;
-    int pkb;             // chain-count bits packed into R's top (front_pkb), 0: CN array
+    int pkb;             // chain-count bits packed into R's top (front_pkb), 0: CN array, -1: HC only
     uint64_t cn, hc, ev; // parse scratch in X (cn unused when pk); the sort's 512-B table at X
 };
 __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
@@ -578,7 +582,7 @@ struct SmallWave {
         const uint32_t nice = (len - i) < 258 ? (len - i) : 258;
         const uint32_t wi = load4(i);
         const uint32_t hi = hash3(wi);
-        const int r = (int)(PK ? R[i] & ((1u << (16 - PK)) - 1u) : (uint32_t)R[i]);
+        const int r = (int)(PK > 0 ? R[i] & ((1u << (16 - (PK > 0 ? PK : 0))) - 1u) : (uint32_t)R[i]);
         uint32_t examined = kPreCand;
         for (int kb = r - 1 - (int)kPreCand;; kb -= 64) {
             const uint32_t thr = best > b0 ? best : b0;
@@ -643,7 +647,7 @@ struct SmallWave {
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
             const uint32_t j = c0 + l;
             const uint32_t e = j < npos ? M[j] : 0u, e1 = j + 1 < npos ? M[j + 1] : 0u;
-            const uint32_t best = e & 511, q = (e >> 9) & 0x3fffu, best1 = e1 & 511;
+            const uint32_t best = e & 511, q = (e >> 9) & 0x7fffu, best1 = e1 & 511;
             const bool cut = (e >> 31) != 0;
             const bool usable = best >= 4 || (best == 3 && j - q <= 4096); // TOO_FAR
             const bool impr = best < 258 && j + 1 < npos && best1 > best;
@@ -675,7 +679,7 @@ struct SmallWave {
                 if (ok) {
                     lit_run(ntok, p, t - p);
                     ntok += t - p;
-                    if (l == 0) tok[ntok] = ((t - ((et >> 9) & 0x3fffu)) << 16) | (bt - 3);
+                    if (l == 0) tok[ntok] = ((t - ((et >> 9) & 0x7fffu)) << 16) | (bt - 3);
                     ntok++;
                     p = t + bt;
                     continue;
@@ -697,7 +701,7 @@ struct SmallWave {
                 match_length = 2;
                 if (i + 3 <= len && prev_length < 258) {
                     const uint32_t e = rfl(M[i]);
-                    uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
+                    uint32_t m = e & 511, q = (e >> 9) & 0x7fffu;
                     if (e >> 31) {
                         m = search<false>(i, prev_length, len, m, q, &q);
                         count(15);
@@ -750,9 +754,13 @@ struct SmallWave {
     // so position 0 is the first entry of its run).  HC = CN > 0 as bits.
     template <int PK>
     __device__ __forceinline__ void build_cn(uint32_t npos) {
-        constexpr uint32_t RB = 16 - PK, CMAX = PK ? (1u << PK) - 1 : 255u;
+        constexpr uint32_t RB = 16 - (PK > 0 ? PK : 0), CMAX = PK > 0 ? (1u << PK) - 1 : 255u;
         const uint32_t l = (uint32_t)lane_id();
         const uint32_t k0 = rfl((uint32_t)R[0]);
+        if (PK < 0) { // has-candidate bits set by position below (HC as u32 words)
+            for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
+            wave_sync();
+        }
         uint32_t ph = 0xffffffffu, prs = 0; // previous chunk's last hash and run start
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
             const uint32_t k = c0 + l;
@@ -765,19 +773,22 @@ struct SmallWave {
             rs = rs > prs ? rs : prs;
             const uint32_t cnt = k - rs - (rs == k0 && k > rs ? 1u : 0u);
             if (valid) {
-                if (PK) R[p] = (uint16_t)(k | (cnt < CMAX ? cnt : CMAX) << RB);
-                else CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
+                if (PK > 0) R[p] = (uint16_t)(k | (cnt < CMAX ? cnt : CMAX) << RB);
+                else if (PK == 0) CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
+                else if (cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
             }
             ph = readlane(h, 63);
             prs = readlane(rs, 63);
         }
         wave_sync();
-        for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
-            const uint32_t x = c0 + l;
-            const uint64_t m = ballot(x < npos && (PK ? ((uint32_t)R[x] >> RB) : (uint32_t)CN[x]) != 0);
-            if (l == 0) HC[c0 >> 6] = m;
+        if (PK >= 0) {
+            for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+                const uint32_t x = c0 + l;
+                const uint64_t m = ballot(x < npos && (PK > 0 ? ((uint32_t)R[x] >> RB) : (uint32_t)CN[x]) != 0);
+                if (l == 0) HC[c0 >> 6] = m;
+            }
+            wave_sync();
         }
-        wave_sync();
     }
     // results of the current eval: window start p0, evaluated offsets m (uniform) and, in
     // lane j, best | q << 9 | cut << 31 for position p0 + j
@@ -809,16 +820,19 @@ struct SmallWave {
         // SAT: a count field narrower than kPreCand saturates below it; such a position gets
         // kPreCand lanes whose candidates are validated (same hash, inside the array, not NIL) and
         // is marked cut (search() resumes it exactly if the parse needs it)
-        constexpr uint32_t RB = 16 - PK, CMAX = PK ? (1u << PK) - 1 : 255u;
+        constexpr uint32_t RB = 16 - (PK > 0 ? PK : 0), CMAX = PK > 0 ? (1u << PK) - 1 : PK < 0 ? 1u : 255u;
         constexpr bool SAT = CMAX < kPreCand;
         const uint32_t l = (uint32_t)lane_id();
         const uint32_t x = p0 + l;
         const uint32_t xc = x < npos ? x : 0u, x1 = x + 1 < npos ? x + 1 : 0u;
         uint32_t rx = R[xc], cn, cn1;
-        if (PK) {
+        if (PK > 0) {
             cn = rx >> RB;
             rx &= (1u << RB) - 1u;
             cn1 = (uint32_t)R[x1] >> RB;
+        } else if (PK < 0) { // (no counts: 1 = has candidates, SAT)
+            cn = (uint32_t)(HC[xc >> 6] >> (xc & 63)) & 1u;
+            cn1 = (uint32_t)(HC[x1 >> 6] >> (x1 & 63)) & 1u;
         } else {
             cn = CN[xc];
             cn1 = CN[x1];
@@ -884,7 +898,7 @@ struct SmallWave {
         const uint32_t nx = (len - x) < 258 ? (len - x) : 258;
         auto neg = [](uint32_t d) { return d >> 31; }; // 1 iff d < 0 as int (all values here are small)
         uint32_t cutc = (SAT ? (cn == CMAX ? 1u : 0u) : neg(kPreCand - cn)) & neg(best - nx);
-        const uint32_t bq = kk & 0x3fffu, e = best | bq << 9 | cutc << 31;
+        const uint32_t bq = kk & 0x7fffu, e = best | bq << 9 | cutc << 31; // (positions < 32768)
         g.p0 = p0;
         g.m = im;
         g.e = e;
@@ -1089,7 +1103,7 @@ struct SmallWave {
                     // 63 of impr is always clear); positions js .. t - 1 become literals
                     const uint32_t st = sj + (uint32_t)__builtin_ctzll(~(g.impr >> sj)), t = g.p0 + st;
                     const uint32_t e0 = readlane(g.e, (int)st);
-                    const uint32_t b0 = e0 & 511, q0 = (e0 >> 9) & 0x3fffu;
+                    const uint32_t b0 = e0 & 511, q0 = (e0 >> 9) & 0x7fffu;
                     if (sflag((uint32_t)(g.fast >> st) & 1u)) {
                         tb_match(tb, lf, t, ((t - q0) << 16) | (b0 - 3));
                         i = t + b0;
@@ -1114,7 +1128,7 @@ struct SmallWave {
                 }
                 if (sflag((uint32_t)(hcw >> (i & 63)) & 1u)) {
                     const uint32_t e = group_get<PK>(g, i, npos, len);
-                    uint32_t m = e & 511, q = (e >> 9) & 0x3fffu;
+                    uint32_t m = e & 511, q = (e >> 9) & 0x7fffu;
                     if (e >> 31) {
                         stamp(2);
                         m = search<PK>(i, pl, len, m, q, &q);
@@ -1888,6 +1902,7 @@ struct SmallWave {
             PMC_STOP(12, 0)
             ntok = cnp == 6   ? parse_ondemand<6>(npos, len)
                    : cnp == 4 ? parse_ondemand<4>(npos, len)
+                   : cnp < 0  ? parse_ondemand<-1>(npos, len)
                               : parse_ondemand<0>(npos, len);
             PMC_STOP(14, 0)
         } else {

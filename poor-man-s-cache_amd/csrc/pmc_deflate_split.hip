@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
         nx = l == 0 ? atomicAdd(a.cQ, kBatch) : 0u;
         const uint64_t vl = g + (uint64_t)l;
         const uint32_t myl = (uint32_t)l < kBatch && vl < a.count ? a.src_len[a.first + vl] : 0u;
-        uint64_t todo = ballot(myl != 0 && myl <= a.lds_max_len);
+        uint64_t todo = ballot(myl != 0 && myl > a.min_len && myl <= a.lds_max_len);
         while (todo) {
             const int jj = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -75,7 +75,8 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
                 nz += (uint32_t)__builtin_popcountll(ballot(s < kLCodes && f != 0));
             }
             if (l == 0) {
-                a.cN[v] = ntok;
+                // >= 16383 symbols: zlib flushes a block mid-value; the HBM kernel redoes the value
+                a.cN[v] = ntok < kSymsPerBlock ? ntok : kNtokMultiBlock;
                 a.cZ[v] = nz;
             }
         }
@@ -315,7 +316,7 @@ template <int CAP>
 __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC_LDS uint32_t *col,
                             PMC_LDS uint16_t *aux) {
     const uint32_t len = a.src_len[a.first + v];
-    if (len == 0 || len > a.lds_max_len) return;
+    if (len == 0 || len <= a.min_len || len > a.lds_max_len || a.cN[v] == kNtokMultiBlock) return;
     LaneTrees<CAP> t;
     t.hp = col;
     t.blc = aux;
@@ -406,7 +407,8 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
         const bool in = (uint32_t)l < kBatch && vl < a.count;
         const uint32_t myl = in ? a.src_len[a.first + vl] : 0u;
         const uint32_t myn = in ? a.cN[vl] : 0u, myp = in ? a.cP[vl] : 0u;
-        uint64_t todo = ballot(in && myl <= a.lds_max_len);
+        // (the small pass, min_len 0, also answers empty values: rc = INVALID_INPUT below)
+        uint64_t todo = ballot(in && (a.min_len == 0 || myl > a.min_len) && myl <= a.lds_max_len);
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -420,6 +422,10 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
                 continue;
             }
             const uint32_t ntok = readlane(myn, j), plan = readlane(myp, j);
+            if (ntok == kNtokMultiBlock) {
+                if (l == 0) a.rc[gv] = kDeflateRetry;
+                continue;
+            }
             for (uint32_t s = l; s < kSplitRows; s += 64) Ls[s] = a.cL[v * kSplitRows + s];
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
             const int rc = w.run_back(a.src + a.src_off[gv], len, ntok, plan, Ls, a.dst + a.dst_off[gv],

@@ -51,7 +51,15 @@ struct DeflateArgs {
     uint32_t *cZ;  // used literal/length symbols per value (front -> visit order of the trees)
     uint32_t *cO;  // trees kernel visit order (values grouped by cZ), or null
     uint32_t *cQ;  // work counters of the front [0] and back [1] kernels (zeroed per chunk)
+    // split pipeline passes: a pass takes the values with min_len < len <= lds_max_len (the large
+    // pass: 16382 < len <= deflate_big_limit()); HBM kernel: retry != 0 also takes every value
+    // whose rc is kDeflateRetry (a large-pass value of >= 16383 symbols: several DEFLATE blocks)
+    uint64_t min_len;
+    int32_t retry;
 };
+
+constexpr int32_t kDeflateRetry = -7778;     // internal rc: the split pipeline declined the value
+constexpr uint32_t kNtokMultiBlock = 0xffffffffu; // cN marker: >= 16383 symbols
 
 constexpr uint32_t kSplitRows = 336;  // 286 lit/len + 30 dist + 19 bit-length (+1)
 constexpr uint32_t kMergeRows = 572;  // 2 heap entries per merge, <= 285 merges
