@@ -220,27 +220,48 @@ struct LaneTrees {
         uint32_t overflow = 0;
         for (int b = 0; b <= kMaxBits; b++) blc[b * 64] = 0;
         setH(K, 0);
-        for (uint32_t i = K; i >= 1; i--) {
-            const uint32_t L = H(i);
+        // The merge list is read back 8 merges (16 keys) per batch with the next batch in flight:
+        // one dependent global round trip per merge made this replay the kernel's longest wait.
+        constexpr int kB = 8;
+        uint32_t cur[2 * kB], nxt[2 * kB];
+        auto fetch = [&](int hi, uint32_t *d) { // merges hi - 1, hi - 2, ..., hi - kB (those >= 0)
 #pragma unroll
-            for (int c = 1; c >= 0; c--) {
-                const uint32_t key = mg[(2 * (i - 1) + c) * 64], x = key & 1023;
-                uint32_t bits = L + 1;
-                if (bits > (uint32_t)max_length) {
-                    bits = (uint32_t)max_length;
-                    overflow++;
-                }
-                if (x >= (uint32_t)elems) {
-                    setH(x - (uint32_t)elems + 1, bits);
-                } else {
-                    lens[row0 + x] = (uint8_t)bits;
-                    blc[bits * 64]++;
-                    const uint32_t f = key >> 15;
-                    const uint32_t xb = xbits(kind, x);
-                    opt += (int64_t)f * (bits + xb);
-                    if (kind != 2) stat += (int64_t)f * (static_len(kind, x) + xb);
+            for (int t = 0; t < kB; t++) {
+                const int j = hi - 1 - t;
+                d[2 * t] = j >= 0 ? mg[(2 * j + 1) * 64] : 0u;   // m first (zlib's heap[heap_max..] order)
+                d[2 * t + 1] = j >= 0 ? mg[(2 * j) * 64] : 0u;
+            }
+        };
+        fetch((int)K, cur);
+        for (int i0 = (int)K; i0 >= 1; i0 -= kB) {
+            fetch(i0 - kB, nxt);
+#pragma unroll
+            for (int t = 0; t < kB; t++) {
+                const int i = i0 - t;
+                if (i < 1) break;
+                const uint32_t L = H((uint32_t)i);
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    const uint32_t key = cur[2 * t + c], x = key & 1023;
+                    uint32_t bits = L + 1;
+                    if (bits > (uint32_t)max_length) {
+                        bits = (uint32_t)max_length;
+                        overflow++;
+                    }
+                    if (x >= (uint32_t)elems) {
+                        setH(x - (uint32_t)elems + 1, bits);
+                    } else {
+                        lens[row0 + x] = (uint8_t)bits;
+                        blc[bits * 64]++;
+                        const uint32_t f = key >> 15;
+                        const uint32_t xb = xbits(kind, x);
+                        opt += (int64_t)f * (bits + xb);
+                        if (kind != 2) stat += (int64_t)f * (static_len(kind, x) + xb);
+                    }
                 }
             }
+#pragma unroll
+            for (int t = 0; t < 2 * kB; t++) cur[t] = nxt[t];
         }
         if (overflow) {
             int ov = (int)overflow;
