@@ -435,6 +435,26 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
             todo &= todo - 1;
             const uint64_t v = g + (uint64_t)j, gv = a.first + v;
             const uint32_t len = readlane(myl, j);
+            // L2 prefetch of the next value of the batch: one dword per lane touches every 128-byte
+            // line of its source bytes, tokens and code-length row, so this value's work hides the
+            // HBM latency of the next one's loads (the dword is consumed after run_back, when it
+            // has long arrived; one VGPR instead of staging registers).
+            uint32_t pf = 0;
+            if (todo) {
+                const int j2 = __builtin_ctzll(todo);
+                const uint64_t v2 = g + (uint64_t)j2, gv2 = a.first + v2;
+                const uint32_t len2 = readlane(myl, j2), n2 = readlane(myn, j2);
+                const uintptr_t sa = (uintptr_t)(a.src + a.src_off[gv2]), ta = (uintptr_t)(a.cT + v2 * a.cap_len),
+                                la = (uintptr_t)(a.cL + v2 * kSplitRows);
+                const uint32_t ns = (uint32_t)(((sa & 127) + len2 + 127) >> 7),
+                               nt = n2 == kNtokMultiBlock ? 0u : (uint32_t)(((ta & 127) + 4ull * n2 + 127) >> 7),
+                               nl = (uint32_t)(((la & 127) + kSplitRows + 127) >> 7);
+                const uint32_t k = (uint32_t)l;
+                const uintptr_t addr = k < ns ? (sa & ~(uintptr_t)127) + 128ull * k
+                                       : k < ns + nt ? (ta & ~(uintptr_t)127) + 128ull * (k - ns)
+                                                     : (la & ~(uintptr_t)127) + 128ull * (k - ns - nt);
+                if (k < ns + nt + nl) pf = *(PMC_GLB const uint32_t *)addr;
+            }
             if (len == 0) {
                 if (l == 0) {
                     a.rc[gv] = PMC_INVALID_INPUT_DEV;
@@ -455,6 +475,7 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
                 a.rc[gv] = rc;
                 if (rc) a.dst_len[gv] = 0;
             }
+            asm volatile("" ::"v"(pf));
         }
     }
     small_wave_stamps_out(w, a);
