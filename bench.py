@@ -207,8 +207,8 @@ def mix_bench(args):
     ops, 50 % SET (compress a fresh value into the key's slot of a device-resident compressed store)
     and 50 % GET (decompress a previously stored value), seed 7.
 
-    The store is one HBM slab of fixed slots (pmc_gzip_bound(vlen) bytes per key) plus a length per
-    key -- SURVEY §8f2's device-resident store.  Per batch, a random permutation of the key space
+    The store is the library's fixed-slot device slab (pmc_slab_*: pmc_gzip_bound(vlen) bytes per key
+    plus a length per key, SURVEY §8f2's device-resident store).  Per batch, a random permutation of the key space
     gives 32,768 SET keys and 32,768 disjoint GET keys, so op order inside a batch cannot change any
     GET's answer.  The store is prefilled (untimed) with value index k for key k; SET j of batch b
     stores fresh value index K + b*32768 + j.  Every GET is verified afterwards against the value
@@ -229,29 +229,27 @@ def mix_bench(args):
     half = bsz // 2
     nb = args.mix_ops // bsz
     cap = pmc_codec.gzip_bound(vlen)
-    stride = (cap + 15) // 16 * 16
 
     def gen(index, n, dst):
         assert L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), seed, 0, 0, index.data_ptr(), n, vlen,
                                 dst.data_ptr(), sh) == 0
 
     # ---- prefill the store: key k holds value index k ----------------------------------------
-    store = torch.empty(K * stride + 16, dtype=torch.uint8, device=dev)
-    slen = torch.zeros(K, dtype=torch.int32, device=dev)
+    slab = pmc_codec.Slab(ctx, K, vlen)
     ver = torch.arange(K, dtype=torch.int64, device=dev)
     src = torch.empty(K * vlen + 16, dtype=torch.uint8, device=dev)
     gen(ver, K, src)
-    koff = torch.arange(K, dtype=torch.int64, device=dev) * stride
     rc = torch.zeros(K, dtype=torch.int32, device=dev)
-    ctx.compress_device(src, koff // stride * vlen, torch.full((K,), vlen, dtype=torch.int32, device=dev), store,
-                        koff, torch.full((K,), cap, dtype=torch.int32, device=dev), slen, rc, vlen, sh)
+    slab.set(src, torch.arange(K, dtype=torch.int64, device=dev) * vlen,
+             torch.full((K,), vlen, dtype=torch.int32, device=dev), torch.arange(K, dtype=torch.int32, device=dev), rc,
+             sh)
     torch.cuda.synchronize()
     assert int((rc != 0).sum()) == 0
     del src
 
     # ---- per-batch inputs (untimed): keys, fresh SET values ---------------------------------
     g = torch.Generator(device="cpu").manual_seed(7)
-    perms = [torch.randperm(K, generator=g)[:bsz].to(dev) for _ in range(nb)]
+    perms = [torch.randperm(K, generator=g)[:bsz].to(dev).to(torch.int32) for _ in range(nb)]
     set_keys = [p[:half].contiguous() for p in perms]
     get_keys = [p[half:].contiguous() for p in perms]
     set_idx = [K + b * half + torch.arange(half, dtype=torch.int64, device=dev) for b in range(nb)]
@@ -260,8 +258,6 @@ def mix_bench(args):
         gen(set_idx[b], half, set_vals[b * half * vlen:])
     v_off = torch.arange(half, dtype=torch.int64, device=dev) * vlen
     v_len = torch.full((half,), vlen, dtype=torch.int32, device=dev)
-    v_cap = torch.full((half,), cap, dtype=torch.int32, device=dev)
-    t_len = torch.zeros(half, dtype=torch.int32, device=dev)
     s_rc = torch.zeros(nb, half, dtype=torch.int32, device=dev)
     outs = torch.empty(nb * half * vlen + 16, dtype=torch.uint8, device=dev)
     o_len = torch.zeros(nb, half, dtype=torch.int32, device=dev)
@@ -283,24 +279,20 @@ def mix_bench(args):
         if b > 0:
             sA.wait_event(evB[b - 1])
         with torch.cuda.stream(sA):
-            # SET: compress the fresh values straight into their keys' store slots
-            ctx.compress_device(set_vals[b * half * vlen:], v_off, v_len, store, sk * stride, v_cap, t_len, s_rc[b],
-                                vlen, sA.cuda_stream)
-            slen[sk] = t_len
-            ver[sk] = set_idx[b]
+            # SET: compress the fresh values straight into their keys' slab slots
+            slab.set(set_vals[b * half * vlen:], v_off, v_len, sk, s_rc[b], sA.cuda_stream)
+            ver[sk.long()] = set_idx[b]
             evA[b].record(sA)
         if b > 0:
             sB.wait_event(evA[b - 1])
         with torch.cuda.stream(sB):
             # GET: decompress the stored members of the GET keys
-            g_ver[b] = ver[gk]
-            ctx.decompress_device(store, gk * stride, slen[gk], outs[b * half * vlen:], v_off, v_len, o_len[b],
-                                  g_rc[b], vlen, sB.cuda_stream)
+            g_ver[b] = ver[gk.long()]
+            slab.get(gk, outs[b * half * vlen:], v_off, v_len, o_len[b], g_rc[b], sB.cuda_stream)
             evB[b].record(sB)
 
     # warm-up GET (untimed): sizes the decompress scratch; its outputs are overwritten by batch 0
-    ctx.decompress_device(store, get_keys[0] * stride, slen[get_keys[0]], outs, v_off, v_len, o_len[0], g_rc[0],
-                          vlen, sh)
+    slab.get(get_keys[0], outs, v_off, v_len, o_len[0], g_rc[0], sh)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
@@ -331,10 +323,12 @@ def mix_bench(args):
         "ms_per_batch": t / nb * 1e3, "higher_is_better": True, "dtype": "u8",
         "data": f"synthetic: JSON slices of the reference's tests/data corpus (seed {seed:#x}), keys seed 7",
         "config": {"workload": f"{K} keys x {vlen} B values, batches of {bsz} ops: 50% SET (compress into the "
-                               "key's HBM slot) / 50% GET (decompress a stored value), disjoint keys per batch",
+                               "key's slot of the device slab, pmc_slab_set) / 50% GET (pmc_slab_get), disjoint "
+                               "keys per batch",
                    "keys": K, "value_bytes": vlen, "batch_ops": bsz,
                    "streams": 1 if args.mix_serial else 2},
         "mismatches": bad}), flush=True)
+    slab.close()
     ctx.close()
 
 

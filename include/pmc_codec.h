@@ -187,6 +187,27 @@ int pmc_store_free(pmc_store *s, pmc_extent *ext, uint32_t n);
 /* used: bytes held by live extents; reserved: heap bytes handed out so far; heap: heap size. */
 int pmc_store_stats(pmc_store *s, uint64_t *used, uint64_t *reserved, uint64_t *heap);
 
+/* ---- fixed-slot device slab (device-resident callers) ---------------------
+ * For callers whose keys, values and bookkeeping already live on the device (bench.py --mix,
+ * BASELINE configs[2]): slot s holds at most one gzip member, at pmc_slab_data() + s * stride
+ * (stride = pmc_gzip_bound(max_value_len) rounded to 16 B), its length in pmc_slab_lengths()[s]
+ * (0 = empty).  All arrays are device pointers; set / get only enqueue on `stream`.
+ *   set: compress value i (src_len[i] <= max_value_len) into slot[i] and record its length (0 on
+ *        failure); the slots of one set call must be distinct.
+ *   get: decompress slot[i] into dst + dst_off[i] (an empty slot gives PMC_INVALID_INPUT).
+ * A set and a get may run concurrently on two streams (the caller orders a get after the set
+ * whose member it must see); two sets (or two gets) on different streams are ordered by the library. */
+typedef struct pmc_slab pmc_slab;
+int pmc_slab_create(pmc_ctx *ctx, uint32_t slots, uint32_t max_value_len, pmc_slab **out);
+void pmc_slab_destroy(pmc_slab *s);
+uint8_t *pmc_slab_data(pmc_slab *s);
+uint32_t *pmc_slab_lengths(pmc_slab *s);
+uint64_t pmc_slab_stride(pmc_slab *s);
+int pmc_slab_set(pmc_slab *s, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                 const uint32_t *slot, uint32_t n, int32_t *rc, void *stream);
+int pmc_slab_get(pmc_slab *s, const uint32_t *slot, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
+                 const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, void *stream);
+
 /* ---- several GPUs from one process -----------------------------------------
  * The reference server is one process that routes key k to shard hashFunc(k) % numShards
  * (/root/reference/src/server/server.cpp:113,121,132).  A group holds one context per entry of

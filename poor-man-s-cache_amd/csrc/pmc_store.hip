@@ -358,3 +358,124 @@ PMC_API int pmc_store_stats(pmc_store *s, uint64_t *used, uint64_t *reserved, ui
     if (heap) *heap = s->heap_bytes;
     return PMC_OK;
 }
+
+// ---- fixed-slot device slab (include/pmc_codec.h pmc_slab_*) ------------------------------------
+// The device-resident form of the store for callers whose keys, values and bookkeeping already live
+// on the device (bench.py --mix, BASELINE configs[2]): slot s holds at most one gzip member at
+// data + s * stride (stride = gzip_bound(max_value_len) rounded to 16 B) and its length in lens[s]
+// (0 = empty).  set / get are enqueue-only batch calls on the caller's stream; the slot layouts are
+// built on the device, so a batch never waits for the host.
+struct pmc_slab {
+    pmc_ctx *ctx = nullptr;
+    uint32_t slots = 0, max_len = 0, cap = 0;
+    uint64_t stride = 0;
+    DevBuf data, lens;
+    DevBuf set_scratch, get_scratch; // per direction: offsets / caps / lengths of a batch
+};
+
+namespace {
+__global__ void slab_set_layout_kernel(const uint32_t *slot, uint32_t n, uint64_t stride, uint32_t cap, uint64_t *doff,
+                                       uint32_t *dcap) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        doff[i] = (uint64_t)slot[i] * stride;
+        dcap[i] = cap;
+    }
+}
+__global__ void slab_commit_kernel(const uint32_t *slot, uint32_t n, const uint32_t *dlen, const int32_t *rc,
+                                   uint32_t *lens) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        lens[slot[i]] = rc[i] == 0 ? dlen[i] : 0u;
+}
+__global__ void slab_get_layout_kernel(const uint32_t *slot, uint32_t n, uint64_t stride, const uint32_t *lens,
+                                       uint64_t *soff, uint32_t *slen) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        soff[i] = (uint64_t)slot[i] * stride;
+        slen[i] = lens[slot[i]];
+    }
+}
+inline dim3 slab_grid(uint32_t n) { return dim3((unsigned)std::min<uint64_t>(((uint64_t)n + 255) / 256, 4096)); }
+} // namespace
+
+PMC_API int pmc_slab_create(pmc_ctx *ctx, uint32_t slots, uint32_t max_value_len, pmc_slab **out) {
+    if (!out) return PMC_E_ARG;
+    *out = nullptr;
+    if (!ctx || !slots || !max_value_len) return PMC_E_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    pmc_slab *s = new pmc_slab;
+    s->ctx = ctx;
+    s->slots = slots;
+    s->max_len = max_value_len;
+    s->cap = (uint32_t)gzip_bound(max_value_len);
+    s->stride = ((uint64_t)s->cap + 15) & ~(uint64_t)15;
+    int r = s->data.ensure(s->stride * slots + 16);
+    if (!r) r = s->lens.ensure((uint64_t)slots * 4);
+    if (!r && hipMemset(s->lens.p, 0, (uint64_t)slots * 4) != hipSuccess) r = PMC_E_NO_DEVICE;
+    if (r) {
+        s->data.release();
+        s->lens.release();
+        delete s;
+        return r;
+    }
+    *out = s;
+    return PMC_OK;
+}
+
+PMC_API void pmc_slab_destroy(pmc_slab *s) {
+    if (!s) return;
+    (void)hipSetDevice(s->ctx->device);
+    (void)hipDeviceSynchronize();
+    s->data.release();
+    s->lens.release();
+    s->set_scratch.release();
+    s->get_scratch.release();
+    delete s;
+}
+
+PMC_API uint8_t *pmc_slab_data(pmc_slab *s) { return s ? (uint8_t *)s->data.p : nullptr; }
+PMC_API uint32_t *pmc_slab_lengths(pmc_slab *s) { return s ? (uint32_t *)s->lens.p : nullptr; }
+PMC_API uint64_t pmc_slab_stride(pmc_slab *s) { return s ? s->stride : 0; }
+
+PMC_API int pmc_slab_set(pmc_slab *s, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                         const uint32_t *slot, uint32_t n, int32_t *rc, void *stream) {
+    if (!s || (n && (!src || !src_off || !src_len || !slot || !rc))) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    pmc_ctx *ctx = s->ctx;
+    hipStream_t st = (hipStream_t)stream;
+    // the set scratch follows the compress direction's ordering (dir_enter / dir_leave)
+    int r = dir_enter(ctx, 0, st);
+    if (r) return r;
+    const uint64_t a8 = ((uint64_t)n * 8 + 255) & ~(uint64_t)255, a4 = ((uint64_t)n * 4 + 255) & ~(uint64_t)255;
+    if ((r = s->set_scratch.ensure(a8 + 2 * a4))) return r;
+    uint64_t *doff = (uint64_t *)s->set_scratch.p;
+    uint32_t *dcap = (uint32_t *)((uint8_t *)doff + a8), *dlen = (uint32_t *)((uint8_t *)dcap + a4);
+    hipLaunchKernelGGL(slab_set_layout_kernel, slab_grid(n), dim3(256), 0, st, slot, n, s->stride, s->cap, doff, dcap);
+    HIP_TRY(hipGetLastError());
+    r = pmc_gzip_compress_batch(ctx, src, src_off, src_len, n, (uint8_t *)s->data.p, doff, dcap, dlen, rc, s->max_len,
+                                stream);
+    if (r) return r;
+    hipLaunchKernelGGL(slab_commit_kernel, slab_grid(n), dim3(256), 0, st, slot, n, (const uint32_t *)dlen,
+                       (const int32_t *)rc, (uint32_t *)s->lens.p);
+    HIP_TRY(hipGetLastError());
+    return dir_leave(ctx, 0, st);
+}
+
+PMC_API int pmc_slab_get(pmc_slab *s, const uint32_t *slot, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
+                         const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, void *stream) {
+    if (!s || (n && (!slot || !dst || !dst_off || !dst_cap || !dst_len || !rc))) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    pmc_ctx *ctx = s->ctx;
+    hipStream_t st = (hipStream_t)stream;
+    int r = dir_enter(ctx, 1, st);
+    if (r) return r;
+    const uint64_t a8 = ((uint64_t)n * 8 + 255) & ~(uint64_t)255;
+    if ((r = s->get_scratch.ensure(a8 + (uint64_t)n * 4 + 256))) return r;
+    uint64_t *soff = (uint64_t *)s->get_scratch.p;
+    uint32_t *slen = (uint32_t *)((uint8_t *)soff + a8);
+    hipLaunchKernelGGL(slab_get_layout_kernel, slab_grid(n), dim3(256), 0, st, slot, n, s->stride,
+                       (const uint32_t *)s->lens.p, soff, slen);
+    HIP_TRY(hipGetLastError());
+    r = pmc_gzip_decompress_batch(ctx, (const uint8_t *)s->data.p, soff, slen, n, dst, dst_off, dst_cap, dst_len, rc,
+                                  s->max_len, stream);
+    if (r) return r;
+    return dir_leave(ctx, 1, st);
+}

@@ -67,6 +67,13 @@ SIGNATURES = {
     "pmc_store_read_members": (_c.c_int, [_p, _p, _u32, _p, _p]),
     "pmc_store_free": (_c.c_int, [_p, _p, _u32]),
     "pmc_store_stats": (_c.c_int, [_p, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_u64)]),
+    "pmc_slab_create": (_c.c_int, [_p, _u32, _u32, _c.POINTER(_p)]),
+    "pmc_slab_destroy": (None, [_p]),
+    "pmc_slab_data": (_p, [_p]),
+    "pmc_slab_lengths": (_p, [_p]),
+    "pmc_slab_stride": (_u64, [_p]),
+    "pmc_slab_set": (_c.c_int, [_p, _p, _p, _p, _p, _u32, _p, _p]),
+    "pmc_slab_get": (_c.c_int, [_p, _p, _u32, _p, _p, _p, _p, _p, _p]),
     "pmc_key_hash": (_u64, [_c.c_char_p, _c.c_size_t]),
     "pmc_group_create": (_c.c_int, [_c.POINTER(_c.c_int), _c.c_int, _c.POINTER(_p)]),
     "pmc_group_destroy": (None, [_p]),
@@ -346,6 +353,49 @@ class Store:
     def close(self):
         if self.handle:
             lib().pmc_store_destroy(self.handle)
+            self.handle = _p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Slab:
+    """Fixed-slot device slab (pmc_slab_*): set(values -> slots), get(slots -> values), all device
+    tensors, enqueue-only on a stream."""
+
+    def __init__(self, ctx: Context, slots: int, max_value_len: int):
+        self.ctx = ctx
+        self.handle = _p()
+        rc = lib().pmc_slab_create(ctx.handle, slots, max_value_len, ctypes.byref(self.handle))
+        if rc != 0:
+            raise CodecUnavailable(f"pmc_slab_create = {rc}: {last_error()}")
+        self.stride = lib().pmc_slab_stride(self.handle)
+        self.slots = slots
+
+    def set(self, src, src_off, src_len, slot, rc, stream=0):
+        r = lib().pmc_slab_set(self.handle, _ptr(src), _ptr(src_off), _ptr(src_len), _ptr(slot), _n(slot), _ptr(rc),
+                               stream)
+        if r != 0:
+            raise CodecUnavailable(f"pmc_slab_set = {r}: {last_error()}")
+
+    def get(self, slot, dst, dst_off, dst_cap, dst_len, rc, stream=0):
+        r = lib().pmc_slab_get(self.handle, _ptr(slot), _n(slot), _ptr(dst), _ptr(dst_off), _ptr(dst_cap),
+                               _ptr(dst_len), _ptr(rc), stream)
+        if r != 0:
+            raise CodecUnavailable(f"pmc_slab_get = {r}: {last_error()}")
+
+    def data_ptr(self):
+        return lib().pmc_slab_data(self.handle)
+
+    def lengths_ptr(self):
+        return lib().pmc_slab_lengths(self.handle)
+
+    def close(self):
+        if self.handle:
+            lib().pmc_slab_destroy(self.handle)
             self.handle = _p()
 
     def __del__(self):

@@ -72,3 +72,79 @@ def test_store_free_reuse_and_full_heap(ctx, golden):
     assert rc3[0] == 0 and rc3[1] == pmc_codec.Z_MEM_ERROR and rc3[2] == 0
     assert [g for _, g in small.get(e3, 3)][0::2] == [b"x" * 100, b"y" * 200]
     assert small.get(e3, 3)[1][0] == pmc_codec.E_ARG
+
+
+def _d2h(ptr, nbytes):
+    """Copy nbytes of device memory at ptr into host bytes (HIP runtime through ctypes)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    buf = ctypes.create_string_buffer(nbytes)
+    assert hip.hipMemcpy(buf, ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes), 2) == 0  # hipMemcpyDeviceToHost
+    return buf.raw
+
+
+def test_slab_set_get_overwrite_empty(ctx, golden):
+    """pmc_slab_*: values into permuted slots (members = the reference's bytes, read back from the slab),
+    get back, overwrite, an empty slot gives INVALID_INPUT."""
+    import numpy as np
+    import torch
+    import pmc_codec
+    from pmc_codec import device as D
+    pairs = [(r, g) for r, g in golden.pairs() if 0 < len(r) <= 4096][:300]
+    n, K = len(pairs), 1000
+    slab = pmc_codec.Slab(ctx, K, 4096)
+    b = D.pack([r for r, _ in pairs])
+    slots = torch.from_numpy(np.random.default_rng(3).permutation(K)[:n].astype(np.int32)).cuda()
+    rc = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    slab.set(b.data, b.off, b.len, slots, rc, D.stream_handle())
+    torch.cuda.synchronize()
+    assert int((rc != 0).sum()) == 0
+    lens = np.frombuffer(_d2h(slab.lengths_ptr(), 4 * K), dtype=np.uint32)
+    data = _d2h(slab.data_ptr(), slab.stride * K)
+    sl = slots.cpu().numpy()
+    for i, (_, g) in enumerate(pairs):
+        assert lens[sl[i]] == len(g) and data[sl[i] * slab.stride:sl[i] * slab.stride + len(g)] == g, i
+    caps = [max(len(r), 1) for r, _ in pairs]
+    dst, doff, dcap = D.slots_for(caps)
+    dlen = torch.zeros(n, dtype=torch.int32, device="cuda")
+    grc = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    slab.get(slots, dst, doff, dcap, dlen, grc, D.stream_handle())
+    torch.cuda.synchronize()
+    assert int((grc != 0).sum()) == 0
+    got = D.Batch(dst, doff, dlen, n, 0).host_items()
+    assert got == [r for r, _ in pairs]
+    # overwrite the first half with the second half's values
+    h = n // 2
+    b2 = D.pack([r for r, _ in pairs[h:2 * h]])
+    rc2 = torch.full((h,), 7, dtype=torch.int32, device="cuda")
+    slab.set(b2.data, b2.off, b2.len, slots[:h].contiguous(), rc2, D.stream_handle())
+    dst2, doff2, dcap2 = D.slots_for([max(len(r), 1) for r, _ in pairs[h:2 * h]])
+    dlen2 = torch.zeros(h, dtype=torch.int32, device="cuda")
+    grc2 = torch.full((h,), 7, dtype=torch.int32, device="cuda")
+    slab.get(slots[:h].contiguous(), dst2, doff2, dcap2, dlen2, grc2, D.stream_handle())
+    torch.cuda.synchronize()
+    assert int((grc2 != 0).sum()) == 0
+    assert D.Batch(dst2, doff2, dlen2, h, 0).host_items() == [r for r, _ in pairs[h:2 * h]]
+    # an empty slot
+    empty = int(np.setdiff1d(np.arange(K), sl)[0])
+    e = torch.tensor([empty], dtype=torch.int32, device="cuda")
+    erc = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+    slab.get(e, dst, doff[:1].contiguous(), dcap[:1].contiguous(), dlen[:1].contiguous(), erc, D.stream_handle())
+    torch.cuda.synchronize()
+    assert int(erc.item()) == pmc_codec.INVALID_INPUT
+    slab.close()
+
+
+def test_mix_bench_two_streams_small():
+    """bench.py --mix (BASELINE configs[2] shape on the slab: SETs and GETs of a batch on two streams,
+    cross-batch order by events), small: every GET verified against the value its key held."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--mix", "--mix-keys", "65536", "--mix-ops",
+                        "262144"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["mismatches"] == 0 and res["config"]["streams"] == 2 and res["ops"] == 262144, res
