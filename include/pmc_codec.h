@@ -270,7 +270,8 @@ int pmc_debug_stamps(pmc_ctx *ctx, uint64_t *dev_buf);
 #define PMC_K_INFLATE_LANE 7   /* lane-per-member decode fast path                     */
 #define PMC_K_INFLATE_VERIFY 8 /* CRC-32 check of the fast path's output               */
 #define PMC_K_ORDER 9          /* lane visit-order counting sorts (trees, lane inflate)  */
-#define PMC_K_COUNT 10
+#define PMC_K_INFLATE_REC 10   /* two-phase record decode of members up to 4 KiB output */
+#define PMC_K_COUNT 11
 int pmc_ctx_profile(pmc_ctx *ctx, int enable);
 int pmc_ctx_kernel_times(pmc_ctx *ctx, double *ms, uint32_t *launches, int nkinds);
 

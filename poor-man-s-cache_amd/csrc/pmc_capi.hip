@@ -169,6 +169,7 @@ struct pmc_ctx {
     DevBuf split;                // chunk arrays of the split small-value pipeline
     DevBuf crcx;                 // inflate: CRC-32 trailers from the lane kernel
     DevBuf order;                // inflate: lane visit order (bins | member indices)
+    DevBuf recs;                 // inflate: the record kernel's per-lane record rows
     // per direction (0 compress, 1 decompress): the event recorded after the last batch call and its
     // stream; a call on another stream waits for it, since both use the direction's scratch
     hipEvent_t dir_ev[2] = {};
@@ -368,6 +369,7 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     c->fbscratch.release();
     c->split.release();
     c->crcx.release();
+    c->recs.release();
     for (auto &r : c->krecs) {
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
@@ -645,9 +647,35 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
             });
             a.order = ord;
         }
+        // members of <= kRecOutMax output bytes: the two-phase record kernel, one block per
+        // resident wave (each block owns 64 record rows); larger ones: the lane kernel
+        static const bool no_rec = getenv("PMC_INFLATE_REC") && !atoi(getenv("PMC_INFLATE_REC"));
         const unsigned lb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * 16);
+        if (!no_rec) {
+            const uint32_t rstride =
+                (uint32_t)std::min<uint64_t>(kRecMax, std::max<uint64_t>(64, ((uint64_t)max_len + 63) & ~(uint64_t)63));
+            // exactly the resident blocks: a block owns its rows for the whole grid-stride loop,
+            // and blocks beyond residency would start only when the first ones have finished
+            static int rec_per_cu = 0;
+            if (!rec_per_cu) {
+                int nb = 0;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)inflate_rec_kernel, 64,
+                                                                 kRecLdsBytes) != hipSuccess || nb < 1)
+                    nb = (int)(kLdsPerCu / kRecLdsBytes);
+                rec_per_cu = nb;
+            }
+            const unsigned rb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * rec_per_cu);
+            r = ctx->recs.ensure((uint64_t)rb * 64 * rstride * 4);
+            if (r) return r;
+            a.rec_scratch = (uint32_t *)ctx->recs.p;
+            a.rec_stride = rstride;
+            klaunch(ctx, PMC_K_INFLATE_REC, st,
+                    [&] { hipLaunchKernelGGL(inflate_rec_kernel, dim3(rb), dim3(64), kRecLdsBytes, st, a); });
+            a.big_only = 1;
+        }
         klaunch(ctx, PMC_K_INFLATE_LANE, st,
                 [&] { hipLaunchKernelGGL(inflate_lane_kernel, dim3(lb), dim3(64), kLaneLdsBytes, st, a); });
+        a.big_only = 0;
         const unsigned vb = (unsigned)std::min<uint64_t>(((uint64_t)n + 511) / 512, (uint64_t)ctx->cus * 4);
         klaunch(ctx, PMC_K_INFLATE_VERIFY, st,
                 [&] { hipLaunchKernelGGL(inflate_verify_kernel, dim3(vb), dim3(512), 0, st, a); });

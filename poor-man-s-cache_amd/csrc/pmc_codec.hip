@@ -5,6 +5,7 @@
 #include "pmc_deflate_split.hip"
 #include "pmc_inflate.hip"
 #include "pmc_inflate_lane.hip"
+#include "pmc_inflate_rec.hip"
 #include "pmc_misc.hip"
 #include "pmc_capi.hip"
 #include "pmc_store.hip"

@@ -450,14 +450,16 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
         const uint32_t in_len = v < a.n ? a.src_len[v] : 0u;
         // st: 0 decoding, 1 end of block reached, 2 declined, 3 no member / empty input
         uint32_t st = v < a.n ? 0u : 3u;
+        if (st == 0 && a.big_only && a.rc[v] != kInflateBig) st = 3; // the record kernel's member
         if (st == 0 && in_len == 0) {
             a.rc[v] = PMC_INVALID_INPUT_DEV;
             a.dst_len[v] = 0;
             st = 3;
         }
+        if (!ballot(st == 0)) continue; // e.g. the pass over the record kernel's large members
         LaneIn in;
         in.p = st == 0 ? a.src + a.src_off[v] : a.src;
-        in.len = in_len;
+        in.len = st == 0 ? in_len : 0u;
         in.blk = (PMC_GLB const uint4 *)((uintptr_t)in.p & ~(uintptr_t)15);
         LaneCode<15> lit, dist;
         lit.base = (PMC_LDS int16_t *)(col + kColBaseL * 64);

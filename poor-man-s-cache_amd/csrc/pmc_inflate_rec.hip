@@ -1,0 +1,458 @@
+// pmc_inflate_rec.hip -- two-phase lane inflate for members whose output fits a 4 KiB image.
+//
+// inflate_lane_kernel decodes one member per lane and copies every match byte by byte
+// through a per-lane ring: a wave iterates once per symbol AND once per 8 match bytes, reads
+// far matches back from dst (a global load that also waits for the ring's earlier stores:
+// gfx9 loads and stores share vmcnt) and holds 40 KB of LDS (4 waves per CU).  Here the
+// work is split by what parallelises (reference: /root/reference/src/compressor/
+// gzip_compressor.cpp:52-111, zlib 1.2.11 inflate_fast):
+//   phase A (lane per member): Huffman-decode the member into RECORDS, one per loop step:
+//     a group of 1-3 literals (bits 31:30 = count, bytes in 23:0) or a match
+//     (bits 31:30 = 0, length - 3 in 7:0, distance - 1 in 22:8).  No byte is produced, so a
+//     step never reads dst; records are staged in LDS and flushed to a per-lane scratch row.
+//     The input window is refilled from registers loaded one half ahead, so its global loads
+//     have a window's worth of steps to land.
+//   phase B (wave per member, the wave's 64 decoded members in turn): a DPP scan of the
+//     records' lengths gives every record its output position; a start bitmap + popcount maps
+//     each output position to its record; a literal position holds its byte, a match
+//     position points distance bytes back; pointer jumping (src[p] = src[src[p]]) resolves
+//     every position to the literal it copies, in log(depth) rounds over LDS; the image goes
+//     to dst with coalesced dword stores.
+// Members of more than kRecOutMax output bytes (by their ISIZE trailer) are left to
+// inflate_lane_kernel (rc = kInflateBig); everything phase A cannot decode exactly is marked
+// kInflateRetry for the wave kernels, as in the lane kernel.  The CRC-32 is checked by
+// inflate_verify_kernel.
+#include <hip/hip_runtime.h>
+
+#include "pmc_device.hpp"
+#include "pmc_kernels.hpp"
+
+namespace pmc {
+
+#ifndef PMC_REC_STAGE
+#define PMC_REC_STAGE 16
+#endif
+constexpr uint32_t kRecStage = PMC_REC_STAGE;         // staged records per lane (LDS column)
+constexpr uint32_t kRecFlushAt = kRecStage * 3 / 4;   // a lane this far behind makes the wave flush
+static_assert((kRecStage & (kRecStage - 1)) == 0 && kRecFlushAt < kRecStage, "stage ring");
+static_assert(kWinDw == 16, "the window prefetch holds one 8-dword half in two uint4");
+// phase A: code columns | input windows | record stage (the build columns live in the last
+// two, which start only after the tables are built)
+constexpr uint32_t kRecWinOff = (uint32_t)kColWords * 64 * 2;
+constexpr uint32_t kRecStageOff = kRecWinOff + kWinDw * 64 * 4;
+constexpr uint32_t kRecLdsBytes = kRecStageOff + kRecStage * 64 * 4;
+static_assert((kBColCl + 19) * 64 * 2 <= (kWinDw + kRecStage) * 64 * 4, "build columns: window + stage");
+// phase B: two output images (16 B of head room so dword -1 reads) | src u16 | start bitmap |
+// per record: its match distance, or 0 for literals (whose bytes go straight to the image)
+constexpr uint32_t kBOut0 = 16;
+constexpr uint32_t kBOut1 = kBOut0 + kRecOutMax + 32;
+constexpr uint32_t kBSrc = kBOut1 + kRecOutMax + 16;
+constexpr uint32_t kBBits = kBSrc + 2 * kRecOutMax;
+constexpr uint32_t kBRecD = kBBits + kRecOutMax / 8;
+static_assert(kBRecD + 2 * kRecMax <= kRecLdsBytes, "phase B reuses phase A's LDS");
+static_assert(kRecOutMax % 1024 == 0, "positions resolve 1024 at a time");
+
+// LaneWin with the next half loaded into registers one advance ahead
+struct LaneWinP {
+    PMC_LDS uint32_t *w;
+    PMC_GLB const uint4 *blk;
+    uint32_t nblk, head, wlo, nd;
+    uint64_t buf;
+    uint32_t n;
+    uint4 pa, pb; // dwords wlo + kWinDw .. + kWinHalf - 1
+    __device__ uint4 block(uint32_t k) const { return k < nblk ? gload16(blk + k) : make_uint4(0, 0, 0, 0); }
+    __device__ void put_half(uint32_t d0, uint4 x, uint4 y) {
+        const uint32_t s0 = d0 & (kWinDw - 1);
+        w[(s0 + 0) * 64] = x.x;
+        w[(s0 + 1) * 64] = x.y;
+        w[(s0 + 2) * 64] = x.z;
+        w[(s0 + 3) * 64] = x.w;
+        w[(s0 + 4) * 64] = y.x;
+        w[(s0 + 5) * 64] = y.y;
+        w[(s0 + 6) * 64] = y.z;
+        w[(s0 + 7) * 64] = y.w;
+    }
+    __device__ void start(const LaneIn &in, uint64_t bp, bool live) {
+        blk = in.blk;
+        head = (uint32_t)(((uintptr_t)in.p & 15) * 8);
+        nblk = live ? (uint32_t)((((uintptr_t)in.p & 15) + in.len + 15) / 16) : 0u;
+        const uint64_t a = bp + head;
+        nd = (uint32_t)(a >> 5);
+        wlo = nd & ~(kWinHalf - 1);
+        const uint4 x0 = block(wlo / 4), x1 = block(wlo / 4 + 1), y0 = block(wlo / 4 + 2), y1 = block(wlo / 4 + 3);
+        pa = block(wlo / 4 + 4);
+        pb = block(wlo / 4 + 5);
+        put_half(wlo, x0, x1);
+        put_half(wlo + kWinHalf, y0, y1);
+        buf = 0;
+        n = 0;
+        refill();
+        drop((uint32_t)(a & 31));
+    }
+    __device__ void refill() {
+        if (n <= 32) {
+            buf |= (uint64_t)w[(nd & (kWinDw - 1)) * 64] << n;
+            n += 32;
+            nd++;
+        }
+    }
+    __device__ bool needs() const { return nd + 4 > wlo + kWinDw; }
+    __device__ void advance() { // retire the consumed older half: the prefetched half takes its slots
+        if (nd >= wlo + kWinHalf) {
+            put_half(wlo + kWinDw, pa, pb);
+            wlo += kWinHalf;
+            pa = block((wlo + kWinDw) / 4);
+            pb = block((wlo + kWinDw) / 4 + 1);
+        }
+    }
+    __device__ uint32_t peek(uint32_t k) const { return (uint32_t)buf & ((1u << k) - 1); }
+    __device__ void drop(uint32_t k) {
+        buf >>= k;
+        n -= k;
+    }
+    __device__ uint32_t bits(uint32_t k) {
+        refill();
+        const uint32_t v = peek(k);
+        drop(k);
+        return v;
+    }
+    __device__ uint64_t bitpos() const { return (uint64_t)nd * 32 - n - head; }
+};
+
+typedef uint32_t rec_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t rec_olen(uint32_t w) { return (w >> 30) ? (w >> 30) : (w & 0xff) + 3; }
+
+__global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint16_t lcol[];
+    uint8_t *lds = (uint8_t *)lcol;
+    const uint32_t lane = threadIdx.x;
+    PMC_LDS uint16_t *col = to_lds<uint16_t>(lcol + lane);
+    PMC_LDS uint32_t *winw = to_lds<uint32_t>((uint32_t *)(lds + kRecWinOff) + lane);
+    PMC_LDS uint32_t *stg = to_lds<uint32_t>((uint32_t *)(lds + kRecStageOff) + lane);
+    PMC_LDS uint16_t *bcol = to_lds<uint16_t>((uint16_t *)(lds + kRecWinOff) + lane);
+    PMC_LDS uint8_t *ob0 = to_lds<uint8_t>(lds + kBOut0), *ob1 = to_lds<uint8_t>(lds + kBOut1);
+    PMC_LDS uint16_t *srcv = to_lds<uint16_t>((uint16_t *)(lds + kBSrc));
+    PMC_LDS uint32_t *bits = to_lds<uint32_t>((uint32_t *)(lds + kBBits));
+    PMC_LDS uint16_t *recd = to_lds<uint16_t>((uint16_t *)(lds + kBRecD));
+    const uint32_t rstride = a.rec_stride;
+    PMC_GLB uint32_t *const rows = (PMC_GLB uint32_t *)a.rec_scratch + (uint64_t)blockIdx.x * 64 * rstride;
+    PMC_GLB uint32_t *const row = rows + (uint64_t)lane * rstride;
+    for (uint64_t vb = (uint64_t)blockIdx.x * 64; vb < a.n; vb += (uint64_t)gridDim.x * 64) {
+        const uint64_t vi = vb + lane;
+        const uint64_t v = a.order && vi < a.n ? (uint64_t)a.order[vi] : vi;
+        const uint32_t in_len = v < a.n ? a.src_len[v] : 0u;
+        // st: 0 decoding, 1 end of block reached, 2 declined, 3 no member / empty input,
+        // 4 output larger than the image (inflate_lane_kernel's)
+        uint32_t st = v < a.n ? 0u : 3u;
+        if (st == 0 && in_len == 0) {
+            a.rc[v] = PMC_INVALID_INPUT_DEV;
+            a.dst_len[v] = 0;
+            st = 3;
+        }
+        LaneIn in;
+        in.p = st == 0 ? a.src + a.src_off[v] : a.src;
+        in.len = st == 0 ? in_len : 0u;
+        in.blk = (PMC_GLB const uint4 *)((uintptr_t)in.p & ~(uintptr_t)15);
+        const uint32_t cap = st == 0 ? a.dst_cap[v] : 0u;
+        const uint64_t dptr = st == 0 ? (uint64_t)(uintptr_t)(a.dst + a.dst_off[v]) : 0u;
+        if (st == 0) {
+            if (in_len < 18) {
+                st = 2;
+            } else {
+                const uint32_t isz = in.byte_at(in_len - 4) | in.byte_at(in_len - 3) << 8 |
+                                     in.byte_at(in_len - 2) << 16 | in.byte_at(in_len - 1) << 24;
+                if (isz > cap) st = 2;
+                else if (isz > kRecOutMax || isz > rstride) st = 4;
+            }
+        }
+        LaneCode<15> lit, dist;
+        lit.base = (PMC_LDS int16_t *)(col + kColBaseL * 64);
+        lit.sym = col + kColLit * 64;
+        dist.base = (PMC_LDS int16_t *)(col + kColBaseD * 64);
+        dist.sym = col + kColDist * 64;
+        bool fixed = false;
+#ifdef PMC_STAMPS
+        uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+        if (st == 0 && !lane_prepare(in, col, bcol, lit, dist, fixed)) st = 2;
+#ifdef PMC_STAMPS
+        uint64_t t1 = __builtin_amdgcn_s_memtime();
+        uint64_t n_it = 0, n_act = 0;
+#endif
+        LaneWinP win;
+        win.w = winw;
+        win.start(in, st == 0 ? in.bitpos() : 0, st == 0);
+        const uint32_t ocap = cap < kRecOutMax ? cap : kRecOutMax;
+        uint32_t pos = 0, nrec = 0, nfl = 0;
+        // ---- phase A: one record per step ----
+        while (ballot(st == 0)) {
+#ifdef PMC_STAMPS
+            n_it++;
+            n_act += __builtin_popcountll(ballot(st == 0));
+#endif
+            if (ballot(st == 0 && win.needs()))
+                if (st == 0) win.advance();
+            if (st == 0) {
+                win.refill();
+                const uint32_t sy = fixed ? fixed_lit(win) : lit.decode(win);
+                uint32_t rec = 0, olen = 0;
+                if (sy < 256) {
+                    // literals are most of the steps: up to three per record (the refilled
+                    // buffer holds >= 17 bits after one code, a full peek)
+                    rec = sy;
+                    olen = 1;
+                    uint32_t l2;
+                    const uint32_t s2 = fixed ? fixed_peek(win, l2) : lit.peek_sym(win, l2);
+                    if (s2 < 256) {
+                        win.drop(l2);
+                        rec |= s2 << 8;
+                        olen = 2;
+                        win.refill();
+                        uint32_t l3;
+                        const uint32_t s3 = fixed ? fixed_peek(win, l3) : lit.peek_sym(win, l3);
+                        if (s3 < 256) {
+                            win.drop(l3);
+                            rec |= s3 << 16;
+                            olen = 3;
+                        }
+                    }
+                    rec |= olen << 30;
+                } else if (sy == 256) {
+                    st = 1;
+                } else if (sy > 285) {
+                    st = 2;
+                } else {
+                    // length / distance bases and extra bits in closed form (RFC 1951 3.2.5)
+                    const uint32_t li = sy - 257;
+                    const uint32_t lx = li < 8 || li == 28 ? 0u : (li - 4) >> 2;
+                    const uint32_t lb = li < 8 ? li + 3 : li == 28 ? 258u : ((4 + (li & 3)) << lx) + 3;
+                    const uint32_t len = lb + win.bits(lx);
+                    win.refill();
+                    const uint32_t ds = fixed ? __builtin_bitreverse32(win.peek(5)) >> 27 : dist.decode(win);
+                    if (fixed) win.drop(5);
+                    const uint32_t dx = ds < 4 ? 0u : (ds >> 1) - 1;
+                    const uint32_t db = ds < 4 ? ds + 1 : ((2 + (ds & 1)) << dx) + 1;
+                    const uint32_t d = db + win.bits(dx < 14 ? dx : 0u);
+                    if (ds > 29 || d > pos) st = 2;
+                    rec = (len - 3) | (d - 1) << 8;
+                    olen = len;
+                }
+                if (st == 0) {
+                    if (pos + olen > ocap || nrec >= rstride) {
+                        st = 2;
+                    } else {
+                        stg[(nrec & (kRecStage - 1)) * 64] = rec;
+                        nrec++;
+                        pos += olen;
+                    }
+                }
+            }
+            // wave-synchronous flush: the wave stores records a few times per member
+            if (ballot(st == 0 && nrec - nfl >= kRecFlushAt))
+                if (st == 0) {
+                    for (uint32_t k = nfl; k < nrec; k++) row[k] = stg[(k & (kRecStage - 1)) * 64];
+                    nfl = nrec;
+                }
+        }
+#ifdef PMC_STAMPS
+        uint64_t t2 = __builtin_amdgcn_s_memtime();
+#endif
+        if (st == 1 && win.bitpos() > (uint64_t)in.len * 8) st = 2;
+        if (st == 1) {
+            const uint32_t t = (uint32_t)((win.bitpos() + 7) >> 3);
+            if (t + 8 > in.len) {
+                st = 2;
+            } else {
+                const uint32_t isz = in.byte_at(t + 4) | in.byte_at(t + 5) << 8 | in.byte_at(t + 6) << 16 |
+                                     in.byte_at(t + 7) << 24;
+                if (isz != pos) {
+                    st = 2;
+                } else {
+                    for (uint32_t k = nfl; k < nrec; k++) row[k] = stg[(k & (kRecStage - 1)) * 64];
+                    a.crc_expect[v] =
+                        in.byte_at(t) | in.byte_at(t + 1) << 8 | in.byte_at(t + 2) << 16 | in.byte_at(t + 3) << 24;
+                }
+            }
+        }
+        if (st == 2) a.rc[v] = kInflateRetry;
+        if (st == 4) a.rc[v] = kInflateBig;
+        // ---- phase B: the wave rebuilds each decoded member in LDS and stores it ----
+        wave_sync_global(); // rows visible to the whole wave; phase A's LDS is dead from here
+#ifdef PMC_STAMPS
+        uint64_t t2b = __builtin_amdgcn_s_memtime();
+        uint64_t n_jump = 0, n_recs = 0, n_mem = 0;
+#endif
+        // Pipelined per member m: (a) its records (prefetched into registers while m - 1
+        // resolved) become the scan / bitmap tables, (b) the next member's records are
+        // requested, (c) m - 1's image (held in the other LDS image buffer) is stored, (d) m
+        // resolves in LDS.  A wait for (a)'s registers then covers loads and stores issued a
+        // whole member earlier.
+        uint64_t todo = ballot(st == 1);
+        auto rl = [](uint32_t x, int m) { return (uint32_t)__builtin_amdgcn_readlane((int)x, m); };
+        uint32_t rg[4] = {0, 0, 0, 0};
+        auto fetch = [&](int m) {
+            const uint32_t mr = rl(nrec, m);
+            PMC_GLB const uint32_t *mrow = rows + (uint64_t)m * rstride;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t k = lane + 64 * j;
+                rg[j] = k < mr ? mrow[k] : 0u;
+            }
+        };
+        auto store_image = [&](PMC_LDS const uint32_t *imgw, uint64_t dptr, uint32_t osz) {
+            // dst dword k holds positions 4k - a0 .. 4k - a0 + 3
+            PMC_GLB uint8_t *dp = (PMC_GLB uint8_t *)dptr;
+            const uint32_t a0 = (uint32_t)(dptr & 3);
+            PMC_GLB uint32_t *dw = (PMC_GLB uint32_t *)(dptr - a0);
+            const uint32_t ndw = (a0 + osz + 3) / 4;
+            for (uint32_t k = lane; k < ndw; k += 64) {
+                const int32_t q = (int32_t)(4 * k) - (int32_t)a0; // first position of the dword
+                const int32_t j = q >> 2;                          // image dword holding q (j >= -1)
+                const uint32_t lo = imgw[j], hi = imgw[j + 1];
+                const uint32_t x = a0 ? __builtin_amdgcn_alignbyte(hi, lo, 4 - a0) : lo;
+                if (q >= 0 && (uint32_t)q + 4 <= osz) {
+                    dw[k] = x;
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 4; b++) {
+                        const int32_t p = q + b;
+                        if (p >= 0 && (uint32_t)p < osz) dp[p] = (uint8_t)(x >> (8 * b));
+                    }
+                }
+            }
+        };
+        if (todo) fetch(__builtin_ctzll(todo));
+        bool p_live = false; // the previous member's image waits in buffer buf ^ 1
+        uint32_t p_osz = 0, buf = 0;
+        uint64_t p_dst = 0, p_v = 0;
+        while (todo) {
+            const int m = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t mrec = rl(nrec, m), osz = rl(pos, m);
+            const uint64_t mv = (uint64_t)rl((uint32_t)v, m) | (uint64_t)rl((uint32_t)(v >> 32), m) << 32;
+            const uint64_t mdst = (uint64_t)rl((uint32_t)dptr, m) | (uint64_t)rl((uint32_t)(dptr >> 32), m) << 32;
+            PMC_GLB const uint32_t *mrow = rows + (uint64_t)m * rstride;
+            PMC_LDS uint8_t *ob = buf ? ob1 : ob0;
+            // (a) record starts: scan of the records' output lengths; bitmap of the starts
+            for (uint32_t k = lane; k < (osz + 31) / 32; k += 64) bits[k] = 0;
+            wave_sync();
+            uint32_t carry = 0;
+            for (uint32_t k0 = 0; k0 < mrec; k0 += 64) {
+                const uint32_t k = k0 + lane, j = k0 / 64;
+                const uint32_t w = j == 0 ? rg[0] : j == 1 ? rg[1] : j == 2 ? rg[2] : j == 3 ? rg[3]
+                                 : k < mrec ? mrow[k] : 0u;
+                const uint32_t ol = k < mrec ? rec_olen(w) : 0u;
+                const uint32_t incl = wave_incl_scan_dpp(ol) + carry;
+                const uint32_t s = incl - ol;
+                if (k < mrec) {
+                    // a literal record places its bytes now; a match keeps its distance
+                    const uint32_t nl = w >> 30;
+                    recd[k] = (uint16_t)(nl ? 0u : ((w >> 8) & 0x7fff) + 1);
+                    lds_or(&bits[s >> 5], 1u << (s & 31));
+                    if (nl) ob[s] = (uint8_t)w;
+                    if (nl >= 2) ob[s + 1] = (uint8_t)(w >> 8);
+                    if (nl == 3) ob[s + 2] = (uint8_t)(w >> 16);
+                }
+                carry = rl(incl, 63);
+            }
+            wave_sync();
+            // (b) the next member's records; (c) the previous member's image
+            if (todo) fetch(__builtin_ctzll(todo));
+            if (p_live) {
+                store_image((PMC_LDS const uint32_t *)(buf ? ob0 : ob1), p_dst, p_osz);
+                if (lane == 0) {
+                    a.dst_len[p_v] = p_osz;
+                    a.rc[p_v] = 0;
+                }
+            }
+            // (d) positions, 1024 per round (16 per lane): record, literal byte or source position
+            uint32_t before = 0;
+            for (uint32_t c0 = 0; c0 < osz; c0 += 1024) {
+                const uint32_t p0 = c0 + 16 * lane;
+                const uint32_t bw = p0 < osz ? (bits[p0 >> 5] >> (p0 & 16)) & 0xffffu : 0u;
+                const uint32_t cnt = (uint32_t)__builtin_popcount(bw);
+                const uint32_t incl = wave_incl_scan_dpp(cnt);
+                const uint32_t base = before + incl - cnt; // record starts before p0
+                before += rl(incl, 63);
+                uint32_t sp[16];
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const uint32_t pr = base + (uint32_t)__builtin_popcount(bw & ((2u << i) - 1));
+                    sp[i] = recd[pr ? pr - 1 : 0u];
+                }
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const uint32_t p = p0 + i;
+                    sp[i] = p < osz && sp[i] ? p - sp[i] : p;
+                }
+                uint32_t sw[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) sw[i] = sp[2 * i] | sp[2 * i + 1] << 16;
+                *(PMC_LDS rec_v4u *)(srcv + p0) = rec_v4u{sw[0], sw[1], sw[2], sw[3]};
+                *(PMC_LDS rec_v4u *)(srcv + p0 + 8) = rec_v4u{sw[4], sw[5], sw[6], sw[7]};
+                wave_sync();
+                // pointer jumping: every position ends at the literal it copies (a literal,
+                // and a position past the end, points at itself)
+                for (;;) {
+                    uint32_t t[16];
+#pragma unroll
+                    for (int i = 0; i < 16; i++) t[i] = srcv[sp[i]];
+                    bool ch = false;
+#pragma unroll
+                    for (int i = 0; i < 16; i++) {
+                        ch |= t[i] != sp[i];
+                        sp[i] = t[i];
+                    }
+                    if (!ballot(ch)) break;
+#ifdef PMC_STAMPS
+                    n_jump++;
+#endif
+#pragma unroll
+                    for (int i = 0; i < 8; i++) sw[i] = sp[2 * i] | sp[2 * i + 1] << 16;
+                    *(PMC_LDS rec_v4u *)(srcv + p0) = rec_v4u{sw[0], sw[1], sw[2], sw[3]};
+                    *(PMC_LDS rec_v4u *)(srcv + p0 + 8) = rec_v4u{sw[4], sw[5], sw[6], sw[7]};
+                    wave_sync();
+                }
+                uint32_t g[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int i = 0; i < 16; i++) g[i >> 2] |= (uint32_t)ob[sp[i]] << (8 * (i & 3));
+                wave_sync();
+                *(PMC_LDS rec_v4u *)(ob + p0) = rec_v4u{g[0], g[1], g[2], g[3]};
+                wave_sync();
+            }
+#ifdef PMC_STAMPS
+            n_recs += mrec;
+            n_mem++;
+#endif
+            p_live = true;
+            p_osz = osz;
+            p_dst = mdst;
+            p_v = mv;
+            buf ^= 1;
+        }
+        if (p_live) {
+            store_image((PMC_LDS const uint32_t *)(buf ? ob0 : ob1), p_dst, p_osz);
+            if (lane == 0) {
+                a.dst_len[p_v] = p_osz;
+                a.rc[p_v] = 0;
+            }
+        }
+        wave_sync();
+#ifdef PMC_STAMPS
+        uint64_t t3 = __builtin_amdgcn_s_memtime();
+        if (threadIdx.x == 0 && a.dbg) {
+            atomicAdd((unsigned long long *)&a.dbg[3], (unsigned long long)n_it);
+            atomicAdd((unsigned long long *)&a.dbg[4], (unsigned long long)n_act);
+            atomicAdd((unsigned long long *)&a.dbg[5], (unsigned long long)(t1 - t0));
+            atomicAdd((unsigned long long *)&a.dbg[6], (unsigned long long)(t2 - t1));
+            atomicAdd((unsigned long long *)&a.dbg[7], (unsigned long long)(t2b - t2));
+            atomicAdd((unsigned long long *)&a.dbg[8], (unsigned long long)(t3 - t2b));
+            atomicAdd((unsigned long long *)&a.dbg[9], (unsigned long long)n_jump);
+            atomicAdd((unsigned long long *)&a.dbg[10], (unsigned long long)n_recs);
+            atomicAdd((unsigned long long *)&a.dbg[11], (unsigned long long)n_mem);
+        }
+#endif
+    }
+}
+
+} // namespace pmc

@@ -92,6 +92,9 @@ struct InflateArgs {
     uint32_t *crc_expect; // lane kernel -> verify kernel: the member's CRC-32 trailer
     int32_t retry_only;   // wave kernels: only members the lane kernel marked kInflateRetry
     const uint32_t *order; // lane kernel: member visit order (by compressed length), or null
+    uint32_t *rec_scratch; // record kernel: per-lane record rows (gridDim * 64 rows of rec_stride words)
+    uint32_t rec_stride;   // records per row (<= kRecMax)
+    int32_t big_only;      // lane kernel: only members the record kernel marked kInflateBig
 };
 
 // lane-inflate visit order: member indices grouped by compressed length, so a wave's 64
@@ -102,6 +105,9 @@ __global__ void order_scan_kernel(uint32_t *hist);
 __global__ void order_scatter_kernel(const uint32_t *src_len, uint64_t n, uint32_t *cursor, uint32_t *order);
 
 constexpr int32_t kInflateRetry = -7777; // internal rc: lane fast path declined the member
+constexpr int32_t kInflateBig = -7779;   // internal rc: output beyond the record kernel's image
+constexpr uint32_t kRecOutMax = 4096;    // record kernel: output image bytes per member
+constexpr uint32_t kRecMax = 2048;       // record kernel: records per member (scratch row)
 
 uint64_t deflate_wave_bytes(bool hbm, uint64_t n);
 uint64_t deflate_small_wave_bytes(uint64_t n);
@@ -119,6 +125,7 @@ __global__ void deflate_back_kernel(DeflateArgs a);
 template <bool kHbm>
 __global__ void inflate_kernel(InflateArgs a);
 __global__ void inflate_lane_kernel(InflateArgs a);
+__global__ void inflate_rec_kernel(InflateArgs a);
 __global__ void inflate_verify_kernel(InflateArgs a);
 __global__ void arg_check_kernel(const uint32_t *src_len, uint64_t n, uint64_t max_len, int32_t *rc,
                                  uint32_t *dst_len);

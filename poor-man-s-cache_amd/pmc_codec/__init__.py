@@ -92,12 +92,13 @@ SIGNATURES = {
 
 # pmc_ctx_kernel_times kinds (include/pmc_codec.h PMC_K_*)
 KERNEL_KINDS = ["deflate_front", "deflate_trees", "deflate_back", "deflate_mono", "deflate_hbm", "inflate_lds",
-                "inflate_hbm", "inflate_lane", "inflate_verify", "order"]
+                "inflate_hbm", "inflate_lane", "inflate_verify", "order", "inflate_rec"]
 KERNEL_NAMES = {"deflate_front": "pmc::deflate_front_kernel", "deflate_trees": "pmc::deflate_trees_kernel",
                 "deflate_back": "pmc::deflate_back_kernel", "deflate_mono": "pmc::deflate_small_kernel",
                 "deflate_hbm": "pmc::deflate_kernel<true>", "inflate_lds": "pmc::inflate_kernel<false>",
                 "inflate_hbm": "pmc::inflate_kernel<true>", "inflate_lane": "pmc::inflate_lane_kernel",
-                "inflate_verify": "pmc::inflate_verify_kernel", "order": "pmc::order_{hist,scan,scatter}_kernel"}
+                "inflate_verify": "pmc::inflate_verify_kernel", "order": "pmc::order_{hist,scan,scatter}_kernel",
+                "inflate_rec": "pmc::inflate_rec_kernel"}
 
 
 def lib():

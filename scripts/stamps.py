@@ -20,8 +20,9 @@ PHASES = ["stage+crc", "hash+sort", "parse", "trees lit+dist (rest)", "emit", "t
           "#parse steps", "#search calls"]
 COUNTS = {7, 8, 9, 13, 14, 15}
 IPHASES = ["inf:stage+header", "inf:block hdr+code lens", "inf:table builds", "lane:#decode iters (wave)",
-           "lane:#active lane-iters", "lane:prepare", "lane:decode loop", "lane:finish"]
-ICOUNTS = {3, 4}
+           "lane:#active lane-iters", "lane:prepare", "lane:decode loop", "lane:finish",
+           "rec:phase B", "rec:#jump rounds", "rec:#records", "rec:#members"]
+ICOUNTS = {3, 4, 9, 10, 11}
 
 
 def main():
