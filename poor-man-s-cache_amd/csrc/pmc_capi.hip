@@ -669,6 +669,9 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
             if (r) return r;
             a.rec_scratch = (uint32_t *)ctx->recs.p;
             a.rec_stride = rstride;
+#if defined(PMC_STAMPS) || defined(PMC_PHASE_STOP)
+            if (const char *e = getenv("PMC_STOP_AFTER")) a.stop_after = atoi(e); // 31 prepare, 32 phase A
+#endif
             klaunch(ctx, PMC_K_INFLATE_REC, st,
                     [&] { hipLaunchKernelGGL(inflate_rec_kernel, dim3(rb), dim3(64), kRecLdsBytes, st, a); });
             a.big_only = 1;

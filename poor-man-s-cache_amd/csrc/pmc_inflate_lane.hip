@@ -183,9 +183,13 @@ struct LaneWin {
 
 // One canonical code of up to 15-bit lengths: per-length limits in registers, bases and the
 // sorted symbol list in the lane's LDS column.
+typedef uint16_t lane_u16x2 __attribute__((ext_vector_type(2)));
 template <int NL>
 struct LaneCode {
-    uint32_t lim[NL]; // left-justified (15-bit) end of the codes of length j + 1
+    static_assert(NL % 2 == 1, "the NL - 1 limits are compared two at a time");
+    // left-justified (15-bit) ends of the codes of length j + 1, j < NL - 1, two per register
+    // (limit 2k in the low half, 2k + 1 in the high half)
+    uint32_t limp[(NL - 1) / 2];
     PMC_LDS int16_t *base;
     PMC_LDS uint16_t *sym;
     // from counts cnt[1..NL] (LDS column); returns false unless the code is complete
@@ -197,20 +201,35 @@ struct LaneCode {
             const int32_t c = cnt[L * 64];
             base[L * 64] = (int16_t)(offs - first);
             first += c;
-            lim[L - 1] = (uint32_t)first << (15 - L);
+            if (L < NL) {
+                const uint32_t lim = (uint32_t)first << (15 - L); // <= 1 << 15
+                if ((L - 1) & 1) limp[(L - 1) / 2] |= lim << 16;
+                else limp[(L - 1) / 2] = lim;
+            }
             first <<= 1;
             offs += c;
             left = (left << 1) - c;
         }
         return left == 0;
     }
+    // code length of the left-justified 15-bit code x: 1 + the number of limits <= x.  x - lim
+    // in 16 bits has bit 15 set exactly when x < lim (both <= 1 << 15), so one packed subtract
+    // tests two limits; the sign bits gather into one word and a popcount counts them.
+    __device__ uint32_t code_len(uint32_t x) const {
+        const uint32_t xx = x | x << 16;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < (NL - 1) / 2; k++) {
+            const lane_u16x2 d = __builtin_bit_cast(lane_u16x2, xx) - __builtin_bit_cast(lane_u16x2, limp[k]);
+            acc |= (__builtin_bit_cast(uint32_t, d) >> k) & (0x80008000u >> k);
+        }
+        return (uint32_t)NL - (uint32_t)__builtin_popcount(acc);
+    }
     // symbol at the head of the bit buffer without consuming it; *len = its code length
     template <class R>
     __device__ uint32_t peek_sym(const R &in, uint32_t &len) const {
         const uint32_t x = __builtin_bitreverse32(in.peek(15)) >> 17;
-        uint32_t L = 1;
-#pragma unroll
-        for (int j = 0; j < NL - 1; j++) L += x >= lim[j] ? 1u : 0u;
+        const uint32_t L = code_len(x);
         const int idx = (int)base[L * 64] + (int)(x >> (15 - L));
         len = L;
         return sym[idx * 64];
@@ -218,9 +237,7 @@ struct LaneCode {
     template <class R>
     __device__ uint32_t decode(R &in) const {
         const uint32_t x = __builtin_bitreverse32(in.peek(15)) >> 17;
-        uint32_t L = 1;
-#pragma unroll
-        for (int j = 0; j < NL - 1; j++) L += x >= lim[j] ? 1u : 0u;
+        const uint32_t L = code_len(x);
         const int idx = (int)base[L * 64] + (int)(x >> (15 - L));
         in.drop(L);
         return sym[idx * 64];

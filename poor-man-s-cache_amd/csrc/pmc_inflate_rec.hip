@@ -46,7 +46,7 @@ static_assert((kBColCl + 19) * 64 * 2 <= (kWinDw + kRecStage) * 64 * 4, "build c
 // per record: its match distance, or 0 for literals (whose bytes go straight to the image)
 constexpr uint32_t kBOut0 = 16;
 constexpr uint32_t kBOut1 = kBOut0 + kRecOutMax + 32;
-constexpr uint32_t kBSrc = kBOut1 + kRecOutMax + 16;
+constexpr uint32_t kBSrc = kBOut1 + kRecOutMax + 32;
 constexpr uint32_t kBBits = kBSrc + 2 * kRecOutMax;
 constexpr uint32_t kBRecD = kBBits + kRecOutMax / 8;
 static_assert(kBRecD + 2 * kRecMax <= kRecLdsBytes, "phase B reuses phase A's LDS");
@@ -179,6 +179,9 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
         uint64_t t1 = __builtin_amdgcn_s_memtime();
         uint64_t n_it = 0, n_act = 0;
 #endif
+#if defined(PMC_STAMPS) || defined(PMC_PHASE_STOP)
+        if (a.stop_after == 31 && st == 0) st = 3;
+#endif
         LaneWinP win;
         win.w = winw;
         win.start(in, st == 0 ? in.bitpos() : 0, st == 0);
@@ -288,6 +291,9 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
         // resolves in LDS.  A wait for (a)'s registers then covers loads and stores issued a
         // whole member earlier.
         uint64_t todo = ballot(st == 1);
+#if defined(PMC_STAMPS) || defined(PMC_PHASE_STOP)
+        if (a.stop_after == 32) todo = 0;
+#endif
         auto rl = [](uint32_t x, int m) { return (uint32_t)__builtin_amdgcn_readlane((int)x, m); };
         uint32_t rg[4] = {0, 0, 0, 0};
         auto fetch = [&](int m) {
@@ -300,23 +306,35 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
             }
         };
         auto store_image = [&](PMC_LDS const uint32_t *imgw, uint64_t dptr, uint32_t osz) {
-            // dst dword k holds positions 4k - a0 .. 4k - a0 + 3
+            // dst dword k holds positions 4k - a0 .. 4k - a0 + 3; a lane stores 4 dwords at once
             PMC_GLB uint8_t *dp = (PMC_GLB uint8_t *)dptr;
             const uint32_t a0 = (uint32_t)(dptr & 3);
             PMC_GLB uint32_t *dw = (PMC_GLB uint32_t *)(dptr - a0);
             const uint32_t ndw = (a0 + osz + 3) / 4;
-            for (uint32_t k = lane; k < ndw; k += 64) {
-                const int32_t q = (int32_t)(4 * k) - (int32_t)a0; // first position of the dword
+            for (uint32_t k = 4 * lane; k < ndw; k += 256) {
+                const int32_t q = (int32_t)(4 * k) - (int32_t)a0; // first position of dword k
                 const int32_t j = q >> 2;                          // image dword holding q (j >= -1)
-                const uint32_t lo = imgw[j], hi = imgw[j + 1];
-                const uint32_t x = a0 ? __builtin_amdgcn_alignbyte(hi, lo, 4 - a0) : lo;
-                if (q >= 0 && (uint32_t)q + 4 <= osz) {
-                    dw[k] = x;
+                uint32_t w[5], x[4];
+#pragma unroll
+                for (int t = 0; t < 5; t++) w[t] = imgw[j + t];
+#pragma unroll
+                for (int t = 0; t < 4; t++) x[t] = a0 ? __builtin_amdgcn_alignbyte(w[t + 1], w[t], 4 - a0) : w[t];
+                if (q >= 0 && (uint32_t)q + 16 <= osz) {
+                    typedef uint32_t g_v4u __attribute__((ext_vector_type(4)));
+                    *(PMC_GLB g_v4u *)(dw + k) = g_v4u{x[0], x[1], x[2], x[3]};
                 } else {
 #pragma unroll
-                    for (int b = 0; b < 4; b++) {
-                        const int32_t p = q + b;
-                        if (p >= 0 && (uint32_t)p < osz) dp[p] = (uint8_t)(x >> (8 * b));
+                    for (int t = 0; t < 4; t++) {
+                        const int32_t qt = q + 4 * t;
+                        if (qt >= 0 && (uint32_t)qt + 4 <= osz) {
+                            dw[k + t] = x[t];
+                        } else {
+#pragma unroll
+                            for (int b = 0; b < 4; b++) {
+                                const int32_t p = qt + b;
+                                if (p >= 0 && (uint32_t)p < osz) dp[p] = (uint8_t)(x[t] >> (8 * b));
+                            }
+                        }
                     }
                 }
             }
