@@ -24,6 +24,8 @@
 // inflate_verify_kernel.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "pmc_device.hpp"
 #include "pmc_kernels.hpp"
 
@@ -285,26 +287,18 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
         uint64_t t2b = __builtin_amdgcn_s_memtime();
         uint64_t n_jump = 0, n_recs = 0, n_mem = 0;
 #endif
-        // Pipelined per member m: (a) its records (prefetched into registers while m - 1
-        // resolved) become the scan / bitmap tables, (b) the next member's records are
-        // requested, (c) m - 1's image (held in the other LDS image buffer) is stored, (d) m
-        // resolves in LDS.  A wait for (a)'s registers then covers loads and stores issued a
-        // whole member earlier.
+        // Phase B runs in PASSES over the 1024-position image: members of <= 256 output bytes
+        // four at a time (a 256-position slice each), larger ones one at a time.  Pipelined per
+        // pass: (a) its records (prefetched into registers during the previous pass) become the
+        // scan / bitmap tables, (b) the next pass's records are requested, (c) the previous
+        // pass's images (in the other LDS image buffer) are stored, (d) the pass resolves in
+        // LDS.  A wait for (a)'s registers then covers loads and stores issued a pass earlier.
         uint64_t todo = ballot(st == 1);
 #if defined(PMC_STAMPS) || defined(PMC_PHASE_STOP)
         if (a.stop_after == 32) todo = 0;
 #endif
         auto rl = [](uint32_t x, int m) { return (uint32_t)__builtin_amdgcn_readlane((int)x, m); };
-        uint32_t rg[4] = {0, 0, 0, 0};
-        auto fetch = [&](int m) {
-            const uint32_t mr = rl(nrec, m);
-            PMC_GLB const uint32_t *mrow = rows + (uint64_t)m * rstride;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t k = lane + 64 * j;
-                rg[j] = k < mr ? mrow[k] : 0u;
-            }
-        };
+        auto rl64 = [&](uint64_t x, int m) { return (uint64_t)rl((uint32_t)x, m) | (uint64_t)rl((uint32_t)(x >> 32), m) << 32; };
         auto store_image = [&](PMC_LDS const uint32_t *imgw, uint64_t dptr, uint32_t osz) {
             // dst dword k holds positions 4k - a0 .. 4k - a0 + 3; a lane stores 4 dwords at once
             PMC_GLB uint8_t *dp = (PMC_GLB uint8_t *)dptr;
@@ -339,122 +333,184 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                 }
             }
         };
-        if (todo) fetch(__builtin_ctzll(todo));
-        bool p_live = false; // the previous member's image waits in buffer buf ^ 1
-        uint32_t p_osz = 0, buf = 0;
-        uint64_t p_dst = 0, p_v = 0;
-        while (todo) {
-            const int m = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const uint32_t mrec = rl(nrec, m), osz = rl(pos, m);
-            const uint64_t mv = (uint64_t)rl((uint32_t)v, m) | (uint64_t)rl((uint32_t)(v >> 32), m) << 32;
-            const uint64_t mdst = (uint64_t)rl((uint32_t)dptr, m) | (uint64_t)rl((uint32_t)(dptr >> 32), m) << 32;
-            PMC_GLB const uint32_t *mrow = rows + (uint64_t)m * rstride;
-            PMC_LDS uint8_t *ob = buf ? ob1 : ob0;
-            // (a) record starts: scan of the records' output lengths; bitmap of the starts
-            for (uint32_t k = lane; k < (osz + 31) / 32; k += 64) bits[k] = 0;
-            wave_sync();
-            uint32_t carry = 0;
-            for (uint32_t k0 = 0; k0 < mrec; k0 += 64) {
-                const uint32_t k = k0 + lane, j = k0 / 64;
-                const uint32_t w = j == 0 ? rg[0] : j == 1 ? rg[1] : j == 2 ? rg[2] : j == 3 ? rg[3]
-                                 : k < mrec ? mrow[k] : 0u;
-                const uint32_t ol = k < mrec ? rec_olen(w) : 0u;
-                const uint32_t incl = wave_incl_scan_dpp(ol) + carry;
-                const uint32_t s = incl - ol;
-                if (k < mrec) {
-                    // a literal record places its bytes now; a match keeps its distance
-                    const uint32_t nl = w >> 30;
-                    recd[k] = (uint16_t)(nl ? 0u : ((w >> 8) & 0x7fff) + 1);
-                    lds_or(&bits[s >> 5], 1u << (s & 31));
-                    if (nl) ob[s] = (uint8_t)w;
-                    if (nl >= 2) ob[s + 1] = (uint8_t)(w >> 8);
-                    if (nl == 3) ob[s + 2] = (uint8_t)(w >> 16);
-                }
-                carry = rl(incl, 63);
-            }
-            wave_sync();
-            // (b) the next member's records; (c) the previous member's image
-            if (todo) fetch(__builtin_ctzll(todo));
-            if (p_live) {
-                store_image((PMC_LDS const uint32_t *)(buf ? ob0 : ob1), p_dst, p_osz);
-                if (lane == 0) {
-                    a.dst_len[p_v] = p_osz;
-                    a.rc[p_v] = 0;
-                }
-            }
-            // (d) positions, 1024 per round (16 per lane): record, literal byte or source position
-            uint32_t before = 0;
-            for (uint32_t c0 = 0; c0 < osz; c0 += 1024) {
-                const uint32_t p0 = c0 + 16 * lane;
-                const uint32_t bw = p0 < osz ? (bits[p0 >> 5] >> (p0 & 16)) & 0xffffu : 0u;
-                const uint32_t cnt = (uint32_t)__builtin_popcount(bw);
-                const uint32_t incl = wave_incl_scan_dpp(cnt);
-                const uint32_t base = before + incl - cnt; // record starts before p0
-                before += rl(incl, 63);
-                uint32_t sp[16];
+        uint32_t buf = 0;
+        auto run_passes = [&](auto Gc, uint64_t set) {
+            constexpr int G = decltype(Gc)::value;
+            constexpr uint32_t span = 1024 / G;
+            uint32_t rg[4] = {0, 0, 0, 0};
+            // the next pass: up to G members from t
+            auto plan = [&](uint64_t &t, int *pm) {
 #pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const uint32_t pr = base + (uint32_t)__builtin_popcount(bw & ((2u << i) - 1));
-                    sp[i] = recd[pr ? pr - 1 : 0u];
+                for (int g = 0; g < G; g++) {
+                    pm[g] = t ? __builtin_ctzll(t) : -1;
+                    t &= t - 1;
                 }
+            };
+            auto fetch = [&](const int *pm) {
+                if (G == 1) {
+                    const uint32_t mr = rl(nrec, pm[0]);
+                    PMC_GLB const uint32_t *mrow = rows + (uint64_t)pm[0] * rstride;
 #pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const uint32_t p = p0 + i;
-                    sp[i] = p < osz && sp[i] ? p - sp[i] : p;
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t k = lane + 64 * j;
+                        rg[j] = k < mr ? mrow[k] : 0u;
+                    }
+                } else {
+#pragma unroll
+                    for (int g = 0; g < G; g++) {
+                        rg[g] = 0;
+                        if (pm[g] >= 0 && lane < rl(nrec, pm[g])) rg[g] = rows[(uint64_t)pm[g] * rstride + lane];
+                    }
                 }
-                uint32_t sw[8];
+            };
+            int cm[G], pm[G], nm[G];
+            uint32_t p_osz[G];
+            uint64_t p_dst[G], p_v[G];
 #pragma unroll
-                for (int i = 0; i < 8; i++) sw[i] = sp[2 * i] | sp[2 * i + 1] << 16;
-                *(PMC_LDS rec_v4u *)(srcv + p0) = rec_v4u{sw[0], sw[1], sw[2], sw[3]};
-                *(PMC_LDS rec_v4u *)(srcv + p0 + 8) = rec_v4u{sw[4], sw[5], sw[6], sw[7]};
+            for (int g = 0; g < G; g++) pm[g] = -1;
+            auto flush_prev = [&]() {
+                PMC_LDS const uint32_t *img = (PMC_LDS const uint32_t *)(buf ? ob0 : ob1);
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    if (pm[g] < 0) continue;
+                    store_image(img + (uint32_t)g * span / 4, p_dst[g], p_osz[g]);
+                    if (lane == 0) {
+                        a.dst_len[p_v[g]] = p_osz[g];
+                        a.rc[p_v[g]] = 0;
+                    }
+                }
+            };
+            plan(set, nm);
+            if (nm[0] >= 0) fetch(nm);
+            while (nm[0] >= 0) {
+                uint32_t osz[G], mrec[G];
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    cm[g] = nm[g];
+                    osz[g] = cm[g] >= 0 ? rl(pos, cm[g]) : 0u;
+                    mrec[g] = cm[g] >= 0 ? rl(nrec, cm[g]) : 0u;
+                }
+                PMC_LDS uint8_t *ob = buf ? ob1 : ob0;
+                // (a) record starts: scan of the records' output lengths; bitmap of the starts
+                const uint32_t ext = G == 1 ? osz[0] : 1024u; // image positions of the pass
+                for (uint32_t k = lane; k < (ext + 31) / 32; k += 64) bits[k] = 0;
                 wave_sync();
-                // pointer jumping: every position ends at the literal it copies (a literal,
-                // and a position past the end, points at itself)
-                for (;;) {
-                    uint32_t t[16];
+                uint32_t R = 0;
 #pragma unroll
-                    for (int i = 0; i < 16; i++) t[i] = srcv[sp[i]];
-                    bool ch = false;
+                for (int g = 0; g < G; g++) {
+                    if (cm[g] < 0) continue;
+                    PMC_GLB const uint32_t *mrow = rows + (uint64_t)cm[g] * rstride;
+                    const uint32_t P = (uint32_t)g * span, mr = mrec[g];
+                    uint32_t carry = 0;
+                    for (uint32_t k0 = 0; k0 < mr; k0 += 64) {
+                        const uint32_t k = k0 + lane, j = k0 / 64;
+                        uint32_t w;
+                        if (G == 1) w = j == 0 ? rg[0] : j == 1 ? rg[1] : j == 2 ? rg[2] : j == 3 ? rg[3] : k < mr ? mrow[k] : 0u;
+                        else w = j == 0 ? rg[g] : k < mr ? mrow[k] : 0u;
+                        const uint32_t ol = k < mr ? rec_olen(w) : 0u;
+                        const uint32_t incl = wave_incl_scan_dpp(ol) + carry;
+                        const uint32_t s = P + incl - ol;
+                        if (k < mr) {
+                            // a literal record places its bytes now; a match keeps its distance
+                            const uint32_t nl = w >> 30;
+                            recd[R + k] = (uint16_t)(nl ? 0u : ((w >> 8) & 0x7fff) + 1);
+                            lds_or(&bits[s >> 5], 1u << (s & 31));
+                            if (nl) ob[s] = (uint8_t)w;
+                            if (nl >= 2) ob[s + 1] = (uint8_t)(w >> 8);
+                            if (nl == 3) ob[s + 2] = (uint8_t)(w >> 16);
+                        }
+                        carry = rl(incl, 63);
+                    }
+                    R += mr;
+                }
+                wave_sync();
+                // (b) the next pass's records; (c) the previous pass's images
+                plan(set, nm);
+                if (nm[0] >= 0) fetch(nm);
+                flush_prev();
+                // (d) positions, 1024 per round (16 per lane): record, literal byte or source position
+                uint32_t before = 0;
+                for (uint32_t c0 = 0; c0 < ext; c0 += 1024) {
+                    const uint32_t p0 = c0 + 16 * lane;
+                    // end of the valid positions of the lane's member
+                    uint32_t lim = osz[0];
+                    if (G > 1) {
+                        const uint32_t gl = p0 / span;
+#pragma unroll
+                        for (int g = 1; g < G; g++)
+                            if (gl == (uint32_t)g) lim = osz[g];
+                        lim += gl * span;
+                    }
+                    const uint32_t bw = p0 < lim ? (bits[p0 >> 5] >> (p0 & 16)) & 0xffffu : 0u;
+                    const uint32_t cnt = (uint32_t)__builtin_popcount(bw);
+                    const uint32_t incl = wave_incl_scan_dpp(cnt);
+                    const uint32_t base = before + incl - cnt; // record starts before p0
+                    before += rl(incl, 63);
+                    uint32_t sp[16];
 #pragma unroll
                     for (int i = 0; i < 16; i++) {
-                        ch |= t[i] != sp[i];
-                        sp[i] = t[i];
+                        const uint32_t pr = base + (uint32_t)__builtin_popcount(bw & ((2u << i) - 1));
+                        sp[i] = recd[pr ? pr - 1 : 0u];
                     }
-                    if (!ballot(ch)) break;
-#ifdef PMC_STAMPS
-                    n_jump++;
-#endif
+#pragma unroll
+                    for (int i = 0; i < 16; i++) {
+                        const uint32_t p = p0 + i;
+                        sp[i] = p < lim && sp[i] ? p - sp[i] : p;
+                    }
+                    uint32_t sw[8];
 #pragma unroll
                     for (int i = 0; i < 8; i++) sw[i] = sp[2 * i] | sp[2 * i + 1] << 16;
                     *(PMC_LDS rec_v4u *)(srcv + p0) = rec_v4u{sw[0], sw[1], sw[2], sw[3]};
                     *(PMC_LDS rec_v4u *)(srcv + p0 + 8) = rec_v4u{sw[4], sw[5], sw[6], sw[7]};
                     wave_sync();
-                }
-                uint32_t g[4] = {0, 0, 0, 0};
+                    // pointer jumping: every position ends at the literal it copies (a literal,
+                    // and a position past its member's end, points at itself)
+                    for (;;) {
+                        uint32_t t[16];
 #pragma unroll
-                for (int i = 0; i < 16; i++) g[i >> 2] |= (uint32_t)ob[sp[i]] << (8 * (i & 3));
-                wave_sync();
-                *(PMC_LDS rec_v4u *)(ob + p0) = rec_v4u{g[0], g[1], g[2], g[3]};
-                wave_sync();
-            }
+                        for (int i = 0; i < 16; i++) t[i] = srcv[sp[i]];
+                        bool ch = false;
+#pragma unroll
+                        for (int i = 0; i < 16; i++) {
+                            ch |= t[i] != sp[i];
+                            sp[i] = t[i];
+                        }
+                        if (!ballot(ch)) break;
 #ifdef PMC_STAMPS
-            n_recs += mrec;
-            n_mem++;
+                        n_jump++;
 #endif
-            p_live = true;
-            p_osz = osz;
-            p_dst = mdst;
-            p_v = mv;
-            buf ^= 1;
-        }
-        if (p_live) {
-            store_image((PMC_LDS const uint32_t *)(buf ? ob0 : ob1), p_dst, p_osz);
-            if (lane == 0) {
-                a.dst_len[p_v] = p_osz;
-                a.rc[p_v] = 0;
+#pragma unroll
+                        for (int i = 0; i < 8; i++) sw[i] = sp[2 * i] | sp[2 * i + 1] << 16;
+                        *(PMC_LDS rec_v4u *)(srcv + p0) = rec_v4u{sw[0], sw[1], sw[2], sw[3]};
+                        *(PMC_LDS rec_v4u *)(srcv + p0 + 8) = rec_v4u{sw[4], sw[5], sw[6], sw[7]};
+                        wave_sync();
+                    }
+                    uint32_t gb[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int i = 0; i < 16; i++) gb[i >> 2] |= (uint32_t)ob[sp[i]] << (8 * (i & 3));
+                    wave_sync();
+                    *(PMC_LDS rec_v4u *)(ob + p0) = rec_v4u{gb[0], gb[1], gb[2], gb[3]};
+                    wave_sync();
+                }
+#ifdef PMC_STAMPS
+                n_recs += R;
+#pragma unroll
+                for (int g = 0; g < G; g++) n_mem += cm[g] >= 0;
+#endif
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    pm[g] = cm[g];
+                    p_osz[g] = osz[g];
+                    p_dst[g] = cm[g] >= 0 ? rl64(dptr, cm[g]) : 0u;
+                    p_v[g] = cm[g] >= 0 ? rl64(v, cm[g]) : 0u;
+                }
+                buf ^= 1;
             }
-        }
+            flush_prev();
+        };
+        const uint64_t small = ballot(st == 1 && pos <= 256);
+        run_passes(std::integral_constant<int, 4>{}, small);
+        run_passes(std::integral_constant<int, 1>{}, todo & ~small);
         wave_sync();
 #ifdef PMC_STAMPS
         uint64_t t3 = __builtin_amdgcn_s_memtime();
