@@ -36,6 +36,7 @@ namespace pmc {
 #endif
 constexpr uint32_t kRecStage = PMC_REC_STAGE;         // staged records per lane (LDS column)
 constexpr uint32_t kRecFlushAt = kRecStage * 3 / 4;   // a lane this far behind makes the wave flush
+static_assert(kRecFlushAt + 3 < kRecStage && kRecStage % 4 == 0, "flushes leave < 4 records pending");
 static_assert((kRecStage & (kRecStage - 1)) == 0 && kRecFlushAt < kRecStage, "stage ring");
 static_assert(kWinDw == 16, "the window prefetch holds one 8-dword half in two uint4");
 // phase A: code columns | input windows | record stage (the build columns live in the last
@@ -91,12 +92,12 @@ struct LaneWinP {
         refill();
         drop((uint32_t)(a & 31));
     }
-    __device__ void refill() {
-        if (n <= 32) {
-            buf |= (uint64_t)w[(nd & (kWinDw - 1)) * 64] << n;
-            n += 32;
-            nd++;
-        }
+    __device__ void refill() { // branch-free: the dword is read either way (its slot always exists)
+        const uint32_t x = w[(nd & (kWinDw - 1)) * 64];
+        const uint32_t r = n <= 32 ? 1u : 0u;
+        buf |= r ? (uint64_t)x << n : 0ull;
+        n += 32 * r;
+        nd += r;
     }
     __device__ bool needs() const { return nd + 4 > wlo + kWinDw; }
     __device__ void advance() { // retire the consumed older half: the prefetched half takes its slots
@@ -189,76 +190,89 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
         win.start(in, st == 0 ? in.bitpos() : 0, st == 0);
         const uint32_t ocap = cap < kRecOutMax ? cap : kRecOutMax;
         uint32_t pos = 0, nrec = 0, nfl = 0;
-        // ---- phase A: one record per step ----
-        while (ballot(st == 0)) {
-#ifdef PMC_STAMPS
-            n_it++;
-            n_act += __builtin_popcountll(ballot(st == 0));
-#endif
-            if (ballot(st == 0 && win.needs()))
-                if (st == 0) win.advance();
-            if (st == 0) {
-                win.refill();
-                const uint32_t sy = fixed ? fixed_lit(win) : lit.decode(win);
-                uint32_t rec = 0, olen = 0;
-                if (sy < 256) {
-                    // literals are most of the steps: up to three per record (the refilled
-                    // buffer holds >= 17 bits after one code, a full peek)
-                    rec = sy;
-                    olen = 1;
-                    uint32_t l2;
-                    const uint32_t s2 = fixed ? fixed_peek(win, l2) : lit.peek_sym(win, l2);
-                    if (s2 < 256) {
-                        win.drop(l2);
-                        rec |= s2 << 8;
-                        olen = 2;
-                        win.refill();
-                        uint32_t l3;
-                        const uint32_t s3 = fixed ? fixed_peek(win, l3) : lit.peek_sym(win, l3);
-                        if (s3 < 256) {
-                            win.drop(l3);
-                            rec |= s3 << 16;
-                            olen = 3;
-                        }
-                    }
-                    rec |= olen << 30;
-                } else if (sy == 256) {
-                    st = 1;
-                } else if (sy > 285) {
-                    st = 2;
-                } else {
-                    // length / distance bases and extra bits in closed form (RFC 1951 3.2.5)
-                    const uint32_t li = sy - 257;
-                    const uint32_t lx = li < 8 || li == 28 ? 0u : (li - 4) >> 2;
-                    const uint32_t lb = li < 8 ? li + 3 : li == 28 ? 258u : ((4 + (li & 3)) << lx) + 3;
-                    const uint32_t len = lb + win.bits(lx);
-                    win.refill();
-                    const uint32_t ds = fixed ? __builtin_bitreverse32(win.peek(5)) >> 27 : dist.decode(win);
-                    if (fixed) win.drop(5);
-                    const uint32_t dx = ds < 4 ? 0u : (ds >> 1) - 1;
-                    const uint32_t db = ds < 4 ? ds + 1 : ((2 + (ds & 1)) << dx) + 1;
-                    const uint32_t d = db + win.bits(dx < 14 ? dx : 0u);
-                    if (ds > 29 || d > pos) st = 2;
-                    rec = (len - 3) | (d - 1) << 8;
-                    olen = len;
-                }
+        // ---- phase A: one record per step (a wave without fixed-code members runs the loop
+        // without the fixed-code paths) ----
+        auto phase_a = [&](auto fxc) {
+            constexpr bool FX = decltype(fxc)::value;
+            while (ballot(st == 0)) {
+    #ifdef PMC_STAMPS
+                n_it++;
+                n_act += __builtin_popcountll(ballot(st == 0));
+    #endif
+                if (ballot(st == 0 && win.needs()))
+                    if (st == 0) win.advance();
                 if (st == 0) {
-                    if (pos + olen > ocap || nrec >= rstride) {
+                    win.refill();
+                    const uint32_t sy = FX && fixed ? fixed_lit(win) : lit.decode(win);
+                    uint32_t rec = 0, olen = 0;
+                    if (sy < 256) {
+                        // literals are most of the steps: up to three per record (the refilled
+                        // buffer holds >= 17 bits after one code, a full peek)
+                        rec = sy;
+                        olen = 1;
+                        uint32_t l2;
+                        const uint32_t s2 = FX && fixed ? fixed_peek(win, l2) : lit.peek_sym(win, l2);
+                        if (s2 < 256) {
+                            win.drop(l2);
+                            rec |= s2 << 8;
+                            olen = 2;
+                            win.refill();
+                            uint32_t l3;
+                            const uint32_t s3 = FX && fixed ? fixed_peek(win, l3) : lit.peek_sym(win, l3);
+                            if (s3 < 256) {
+                                win.drop(l3);
+                                rec |= s3 << 16;
+                                olen = 3;
+                            }
+                        }
+                        rec |= olen << 30;
+                    } else if (sy == 256) {
+                        st = 1;
+                    } else if (sy > 285) {
                         st = 2;
                     } else {
-                        stg[(nrec & (kRecStage - 1)) * 64] = rec;
-                        nrec++;
-                        pos += olen;
+                        // length / distance bases and extra bits in closed form (RFC 1951 3.2.5)
+                        const uint32_t li = sy - 257;
+                        const uint32_t lx = li < 8 || li == 28 ? 0u : (li - 4) >> 2;
+                        const uint32_t lb = li < 8 ? li + 3 : li == 28 ? 258u : ((4 + (li & 3)) << lx) + 3;
+                        const uint32_t len = lb + win.bits(lx);
+                        win.refill();
+                        const uint32_t ds = FX && fixed ? __builtin_bitreverse32(win.peek(5)) >> 27 : dist.decode(win);
+                        if (FX && fixed) win.drop(5);
+                        const uint32_t dx = ds < 4 ? 0u : (ds >> 1) - 1;
+                        const uint32_t db = ds < 4 ? ds + 1 : ((2 + (ds & 1)) << dx) + 1;
+                        const uint32_t d = db + win.bits(dx < 14 ? dx : 0u);
+                        if (ds > 29 || d > pos) st = 2;
+                        rec = (len - 3) | (d - 1) << 8;
+                        olen = len;
+                    }
+                    if (st == 0) {
+                        if (pos + olen > ocap || nrec >= rstride) {
+                            st = 2;
+                        } else {
+                            stg[(nrec & (kRecStage - 1)) * 64] = rec;
+                            nrec++;
+                            pos += olen;
+                        }
                     }
                 }
+                // wave-synchronous flush of whole 4-record groups (one 16-byte store each): the
+                // wave stores records a few times per member
+                if (ballot(st == 0 && nrec - nfl >= kRecFlushAt))
+                    if (st == 0) {
+                        const uint32_t e = nrec & ~3u;
+                        for (uint32_t k = nfl; k < e; k += 4) {
+                            typedef uint32_t r_v4u __attribute__((ext_vector_type(4)));
+                            const uint32_t s0 = k & (kRecStage - 1);
+                            *(PMC_GLB r_v4u *)(row + k) = r_v4u{stg[s0 * 64], stg[(s0 + 1) * 64], stg[(s0 + 2) * 64],
+                                                                stg[(s0 + 3) * 64]};
+                        }
+                        nfl = e;
+                    }
             }
-            // wave-synchronous flush: the wave stores records a few times per member
-            if (ballot(st == 0 && nrec - nfl >= kRecFlushAt))
-                if (st == 0) {
-                    for (uint32_t k = nfl; k < nrec; k++) row[k] = stg[(k & (kRecStage - 1)) * 64];
-                    nfl = nrec;
-                }
-        }
+        };
+        if (ballot(st == 0 && fixed)) phase_a(std::true_type{});
+        else phase_a(std::false_type{});
 #ifdef PMC_STAMPS
         uint64_t t2 = __builtin_amdgcn_s_memtime();
 #endif
@@ -508,7 +522,7 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
             }
             flush_prev();
         };
-        const uint64_t small = ballot(st == 1 && pos <= 256);
+        const uint64_t small = todo & ballot(pos <= 256);
         run_passes(std::integral_constant<int, 4>{}, small);
         run_passes(std::integral_constant<int, 1>{}, todo & ~small);
         wave_sync();
