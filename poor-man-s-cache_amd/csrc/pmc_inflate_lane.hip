@@ -32,7 +32,10 @@ constexpr int kLaneLitCap = 96, kLaneDistCap = 32;
 // the output ring's bytes, which are only written once decoding starts.
 constexpr int kColLit = 0, kColDist = kColLit + kLaneLitCap, kColBaseL = kColDist + kLaneDistCap;
 constexpr int kColBaseD = kColBaseL + 16, kColWords = kColBaseD + 16;
-constexpr int kBColCntL = 0, kBColCntD = 16, kBColBaseC = 32, kBColCl = 40; // build columns (+19)
+// build columns (u8 entries, entry i of lane l at byte i * 64 + l): counts / offsets per code length
+// of the lit/len and distance codes (a count above the lists' capacity declines anyway, so 8 bits
+// saturating suffice), the code-length code's bases (int8) and sorted symbols (+19)
+constexpr int kBColCntL = 0, kBColCntD = 16, kBColBaseC = 32, kBColCl = 40;
 #ifndef PMC_LANE_WIN
 #define PMC_LANE_WIN 16
 #endif
@@ -48,7 +51,7 @@ constexpr uint32_t kRing = PMC_LANE_RING, kFlush = kRing / 2;
 constexpr uint32_t kLaneRingOff = (uint32_t)kColWords * 64 * 2;            // output rings (LaneOut)
 constexpr uint32_t kLaneWinOff = kLaneRingOff + kRing / 4 * 64 * 4;        // input windows (LaneWin)
 constexpr uint32_t kLaneLdsBytes = kLaneWinOff + kWinDw * 64 * 4;
-static_assert((kBColCl + 19) * 64 * 2 <= kRing * 64, "build columns live in the output rings");
+static_assert((kBColCl + 19) * 64 <= kRing * 64, "build columns live in the output rings");
 
 // 16-byte load through a global (not flat) pointer: flat loads also count against lgkmcnt,
 // so every LDS wait would wait for them too
@@ -184,22 +187,23 @@ struct LaneWin {
 // One canonical code of up to 15-bit lengths: per-length limits in registers, bases and the
 // sorted symbol list in the lane's LDS column.
 typedef uint16_t lane_u16x2 __attribute__((ext_vector_type(2)));
-template <int NL>
+template <int NL, class BT = int16_t, class ST = uint16_t>
 struct LaneCode {
     static_assert(NL % 2 == 1, "the NL - 1 limits are compared two at a time");
     // left-justified (15-bit) ends of the codes of length j + 1, j < NL - 1, two per register
     // (limit 2k in the low half, 2k + 1 in the high half)
     uint32_t limp[(NL - 1) / 2];
-    PMC_LDS int16_t *base;
-    PMC_LDS uint16_t *sym;
+    PMC_LDS BT *base;
+    PMC_LDS ST *sym;
     // from counts cnt[1..NL] (LDS column); returns false unless the code is complete
     // (every well-formed zlib stream's codes are; other shapes go to the wave kernel)
-    __device__ bool build(PMC_LDS const uint16_t *cnt) {
+    template <class CT>
+    __device__ bool build(PMC_LDS const CT *cnt) {
         int32_t first = 0, offs = 0, left = 1;
 #pragma unroll
         for (int L = 1; L <= NL; L++) {
             const int32_t c = cnt[L * 64];
-            base[L * 64] = (int16_t)(offs - first);
+            base[L * 64] = (BT)(offs - first);
             first += c;
             if (L < NL) {
                 const uint32_t lim = (uint32_t)first << (15 - L); // <= 1 << 15
@@ -287,8 +291,9 @@ __device__ __forceinline__ uint32_t fixed_lit(R &in) {
 // Code lengths of a dynamic block through the code-length code; pass 0 counts them
 // (cnt columns), pass 1 places every symbol into its list (cnt columns hold offsets).
 // Returns false on any malformed sequence.
-__device__ bool lane_lengths(LaneIn &in, const LaneCode<7> &clc, uint32_t nlen, uint32_t nlit, PMC_LDS uint16_t *col,
-                             PMC_LDS uint16_t *bcol, int pass, bool &eob_ok) {
+typedef LaneCode<7, int8_t, uint8_t> LaneClc; // the code-length code, in the byte build columns
+__device__ bool lane_lengths(LaneIn &in, const LaneClc &clc, uint32_t nlen, uint32_t nlit, PMC_LDS uint16_t *col,
+                             PMC_LDS uint8_t *bcol, int pass, bool &eob_ok) {
     uint32_t k = 0, prev = 0;
     while (k < nlen) {
         in.refill();
@@ -312,13 +317,14 @@ __device__ bool lane_lengths(LaneIn &in, const LaneCode<7> &clc, uint32_t nlen, 
         if (val) {
             for (uint32_t r = 0; r < rep; r++, k++) {
                 const bool lit = k < nlit;
-                PMC_LDS uint16_t *c = bcol + (lit ? kBColCntL : kBColCntD) * 64 + val * 64;
+                PMC_LDS uint8_t *c = bcol + (lit ? kBColCntL : kBColCntD) * 64 + val * 64;
                 if (pass == 0) {
-                    *c = (uint16_t)(*c + 1);
+                    const uint32_t x = *c;
+                    *c = (uint8_t)(x < 255 ? x + 1 : 255u);
                     if (k == 256) eob_ok = true;
                 } else {
                     const uint32_t at = *c;
-                    *c = (uint16_t)(at + 1);
+                    *c = (uint8_t)(at + 1);
                     col[((lit ? kColLit : kColDist) + at) * 64] = (uint16_t)(lit ? k : k - nlit);
                 }
             }
@@ -332,7 +338,7 @@ __device__ bool lane_lengths(LaneIn &in, const LaneCode<7> &clc, uint32_t nlen, 
 
 // Header and block header of a single-block fixed/dynamic member, code tables built;
 // false = decline (stored or multi-block members, header flags, malformed codes ...).
-__device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint16_t *bcol, LaneCode<15> &lit,
+__device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
                              LaneCode<15> &dist, bool &fixed) {
     if (in.len < 18) return false;
     if (in.byte_at(0) != 0x1f || in.byte_at(1) != 0x8b || in.byte_at(2) != 8 || in.byte_at(3) != 0) return false;
@@ -349,24 +355,24 @@ __device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint16_t
     for (int L = 0; L < 16; L++) bcol[(kBColCntL + L) * 64] = 0;
     for (uint32_t sy = 0; sy < 19; sy++) {
         const uint32_t L = (uint32_t)(cll >> (3 * sy)) & 7;
-        if (L) bcol[(kBColCntL + L) * 64] = (uint16_t)(bcol[(kBColCntL + L) * 64] + 1);
+        if (L) bcol[(kBColCntL + L) * 64] = (uint8_t)(bcol[(kBColCntL + L) * 64] + 1);
     }
-    LaneCode<7> clc;
-    clc.base = (PMC_LDS int16_t *)(bcol + kBColBaseC * 64);
+    LaneClc clc;
+    clc.base = (PMC_LDS int8_t *)(bcol + kBColBaseC * 64);
     clc.sym = bcol + kBColCl * 64;
     if (!clc.build(bcol + kBColCntL * 64)) return false;
     {
         uint32_t offs = 0;
         for (int L = 1; L < 8; L++) {
             const uint32_t c = bcol[(kBColCntL + L) * 64];
-            bcol[(kBColCntL + L) * 64] = (uint16_t)offs;
+            bcol[(kBColCntL + L) * 64] = (uint8_t)offs;
             offs += c;
         }
         for (uint32_t sy = 0; sy < 19; sy++) {
             const uint32_t L = (uint32_t)(cll >> (3 * sy)) & 7;
             if (L) {
                 const uint32_t at = bcol[(kBColCntL + L) * 64];
-                bcol[(kBColCntL + L) * 64] = (uint16_t)(at + 1);
+                bcol[(kBColCntL + L) * 64] = (uint8_t)(at + 1);
                 clc.sym[at * 64] = (uint16_t)sy;
             }
         }
@@ -391,8 +397,8 @@ __device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint16_t
         uint32_t ol = 0, od = 0;
         for (int L = 1; L < 16; L++) {
             const uint32_t cl = bcol[(kBColCntL + L) * 64], cd = bcol[(kBColCntD + L) * 64];
-            bcol[(kBColCntL + L) * 64] = (uint16_t)ol;
-            bcol[(kBColCntD + L) * 64] = (uint16_t)od;
+            bcol[(kBColCntL + L) * 64] = (uint8_t)ol;
+            bcol[(kBColCntD + L) * 64] = (uint8_t)od;
             ol += cl;
             od += cd;
         }
@@ -459,7 +465,7 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint16_t lcol[];
     PMC_LDS uint16_t *col = to_lds<uint16_t>(lcol + threadIdx.x);
     PMC_LDS uint32_t *ring = to_lds<uint32_t>((uint8_t *)lcol + kLaneRingOff) + threadIdx.x;
-    PMC_LDS uint16_t *bcol = to_lds<uint16_t>((uint16_t *)((uint8_t *)lcol + kLaneRingOff) + threadIdx.x);
+    PMC_LDS uint8_t *bcol = to_lds<uint8_t>((uint8_t *)lcol + kLaneRingOff + threadIdx.x);
     PMC_LDS uint32_t *winw = to_lds<uint32_t>((uint8_t *)lcol + kLaneWinOff) + threadIdx.x;
     for (uint64_t vb = (uint64_t)blockIdx.x * 64; vb < a.n; vb += (uint64_t)gridDim.x * 64) {
         const uint64_t vi = vb + threadIdx.x;

@@ -32,10 +32,10 @@
 namespace pmc {
 
 #ifndef PMC_REC_STAGE
-#define PMC_REC_STAGE 16
+#define PMC_REC_STAGE 8
 #endif
 constexpr uint32_t kRecStage = PMC_REC_STAGE;         // staged records per lane (LDS column)
-constexpr uint32_t kRecFlushAt = kRecStage * 3 / 4;   // a lane this far behind makes the wave flush
+constexpr uint32_t kRecFlushAt = kRecStage - 4;       // a lane this far behind makes the wave flush
 static_assert(kRecFlushAt + 3 < kRecStage && kRecStage % 4 == 0, "flushes leave < 4 records pending");
 static_assert((kRecStage & (kRecStage - 1)) == 0 && kRecFlushAt < kRecStage, "stage ring");
 static_assert(kWinDw == 16, "the window prefetch holds one 8-dword half in two uint4");
@@ -44,7 +44,7 @@ static_assert(kWinDw == 16, "the window prefetch holds one 8-dword half in two u
 constexpr uint32_t kRecWinOff = (uint32_t)kColWords * 64 * 2;
 constexpr uint32_t kRecStageOff = kRecWinOff + kWinDw * 64 * 4;
 constexpr uint32_t kRecLdsBytes = kRecStageOff + kRecStage * 64 * 4;
-static_assert((kBColCl + 19) * 64 * 2 <= (kWinDw + kRecStage) * 64 * 4, "build columns: window + stage");
+static_assert((kBColCl + 19) * 64 <= (kWinDw + kRecStage) * 64 * 4, "build columns: window + stage");
 // phase B: two output images (16 B of head room so dword -1 reads) | src u16 | start bitmap |
 // per record: its match distance, or 0 for literals (whose bytes go straight to the image)
 constexpr uint32_t kBOut0 = 16;
@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
     PMC_LDS uint16_t *col = to_lds<uint16_t>(lcol + lane);
     PMC_LDS uint32_t *winw = to_lds<uint32_t>((uint32_t *)(lds + kRecWinOff) + lane);
     PMC_LDS uint32_t *stg = to_lds<uint32_t>((uint32_t *)(lds + kRecStageOff) + lane);
-    PMC_LDS uint16_t *bcol = to_lds<uint16_t>((uint16_t *)(lds + kRecWinOff) + lane);
+    PMC_LDS uint8_t *bcol = to_lds<uint8_t>(lds + kRecWinOff + lane);
     PMC_LDS uint8_t *ob0 = to_lds<uint8_t>(lds + kBOut0), *ob1 = to_lds<uint8_t>(lds + kBOut1);
     PMC_LDS uint16_t *srcv = to_lds<uint16_t>((uint16_t *)(lds + kBSrc));
     PMC_LDS uint32_t *bits = to_lds<uint32_t>((uint32_t *)(lds + kBBits));
