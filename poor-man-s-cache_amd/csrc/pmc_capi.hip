@@ -665,9 +665,11 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
                 rec_per_cu = nb;
             }
             const unsigned rb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * rec_per_cu);
-            r = ctx->recs.ensure((uint64_t)rb * 64 * rstride * 4);
+            r = ctx->recs.ensure((uint64_t)rb * 64 * rstride * 4 + 256);
             if (r) return r;
-            a.rec_scratch = (uint32_t *)ctx->recs.p;
+            a.rec_work = (uint32_t *)ctx->recs.p;
+            a.rec_scratch = (uint32_t *)((uint8_t *)ctx->recs.p + 256);
+            HIP_TRY(hipMemsetAsync(a.rec_work, 0, 4, st));
             a.rec_stride = rstride;
 #if defined(PMC_STAMPS) || defined(PMC_PHASE_STOP)
             if (const char *e = getenv("PMC_STOP_AFTER")) a.stop_after = atoi(e); // 31 prepare, 32 phase A

@@ -26,12 +26,20 @@
 
 namespace pmc {
 
-constexpr int kLaneLitCap = 96, kLaneDistCap = 32;
+constexpr int kLaneLitCap = 96, kLaneDistCap = 30;
 // per-lane LDS columns (u16 words, entry i of lane l at word i * 64 + l).  Decode-time:
 // symbol lists and bases.  Build-time scratch (counts / offsets, code-length code) lives in
 // the output ring's bytes, which are only written once decoding starts.
-constexpr int kColLit = 0, kColDist = kColLit + kLaneLitCap, kColBaseL = kColDist + kLaneDistCap;
-constexpr int kColBaseD = kColBaseL + 16, kColWords = kColBaseD + 16;
+// (bases: one entry per code length 1..15)
+template <int LIT, int DIST>
+struct LaneCols {
+    static constexpr int kLit = LIT, kDist = DIST;
+    static constexpr int kColLit = 0, kColDist = LIT, kColBaseL = LIT + DIST, kColBaseD = kColBaseL + 15;
+    static constexpr int kColWords = kColBaseD + 15;
+};
+typedef LaneCols<kLaneLitCap, kLaneDistCap> LaneColsL; // the lane kernel's lists
+constexpr int kColLit = LaneColsL::kColLit, kColDist = LaneColsL::kColDist, kColBaseL = LaneColsL::kColBaseL;
+constexpr int kColBaseD = LaneColsL::kColBaseD, kColWords = LaneColsL::kColWords;
 // build columns (u8 entries, entry i of lane l at byte i * 64 + l): counts / offsets per code length
 // of the lit/len and distance codes (a count above the lists' capacity declines anyway, so 8 bits
 // saturating suffice), the code-length code's bases (int8) and sorted symbols (+19)
@@ -203,7 +211,7 @@ struct LaneCode {
 #pragma unroll
         for (int L = 1; L <= NL; L++) {
             const int32_t c = cnt[L * 64];
-            base[L * 64] = (BT)(offs - first);
+            base[(L - 1) * 64] = (BT)(offs - first);
             first += c;
             if (L < NL) {
                 const uint32_t lim = (uint32_t)first << (15 - L); // <= 1 << 15
@@ -234,7 +242,7 @@ struct LaneCode {
     __device__ uint32_t peek_sym(const R &in, uint32_t &len) const {
         const uint32_t x = __builtin_bitreverse32(in.peek(15)) >> 17;
         const uint32_t L = code_len(x);
-        const int idx = (int)base[L * 64] + (int)(x >> (15 - L));
+        const int idx = (int)base[(L - 1) * 64] + (int)(x >> (15 - L));
         len = L;
         return sym[idx * 64];
     }
@@ -242,7 +250,7 @@ struct LaneCode {
     __device__ uint32_t decode(R &in) const {
         const uint32_t x = __builtin_bitreverse32(in.peek(15)) >> 17;
         const uint32_t L = code_len(x);
-        const int idx = (int)base[L * 64] + (int)(x >> (15 - L));
+        const int idx = (int)base[(L - 1) * 64] + (int)(x >> (15 - L));
         in.drop(L);
         return sym[idx * 64];
     }
@@ -292,6 +300,7 @@ __device__ __forceinline__ uint32_t fixed_lit(R &in) {
 // (cnt columns), pass 1 places every symbol into its list (cnt columns hold offsets).
 // Returns false on any malformed sequence.
 typedef LaneCode<7, int8_t, uint8_t> LaneClc; // the code-length code, in the byte build columns
+template <class C>
 __device__ bool lane_lengths(LaneIn &in, const LaneClc &clc, uint32_t nlen, uint32_t nlit, PMC_LDS uint16_t *col,
                              PMC_LDS uint8_t *bcol, int pass, bool &eob_ok) {
     uint32_t k = 0, prev = 0;
@@ -325,7 +334,7 @@ __device__ bool lane_lengths(LaneIn &in, const LaneClc &clc, uint32_t nlen, uint
                 } else {
                     const uint32_t at = *c;
                     *c = (uint8_t)(at + 1);
-                    col[((lit ? kColLit : kColDist) + at) * 64] = (uint16_t)(lit ? k : k - nlit);
+                    col[((lit ? C::kColLit : C::kColDist) + at) * 64] = (uint16_t)(lit ? k : k - nlit);
                 }
             }
         } else {
@@ -337,9 +346,11 @@ __device__ bool lane_lengths(LaneIn &in, const LaneClc &clc, uint32_t nlen, uint
 }
 
 // Header and block header of a single-block fixed/dynamic member, code tables built;
-// false = decline (stored or multi-block members, header flags, malformed codes ...).
+// false = decline (stored or multi-block members, header flags, malformed codes ...).  *over
+// (if given) is set when the only reason is C's list capacity: the lane kernel's lists hold it.
+template <class C>
 __device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
-                             LaneCode<15> &dist, bool &fixed) {
+                             LaneCode<15> &dist, bool &fixed, bool *over = nullptr) {
     if (in.len < 18) return false;
     if (in.byte_at(0) != 0x1f || in.byte_at(1) != 0x8b || in.byte_at(2) != 8 || in.byte_at(3) != 0) return false;
     in.seek(80);
@@ -384,14 +395,17 @@ __device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t 
     }
     const uint64_t lens_at = in.bitpos();
     bool eob_ok = false;
-    if (!lane_lengths(in, clc, nlit + ndist, nlit, col, bcol, 0, eob_ok) || !eob_ok) return false;
+    if (!lane_lengths<C>(in, clc, nlit + ndist, nlit, col, bcol, 0, eob_ok) || !eob_ok) return false;
     const uint64_t data_at = in.bitpos();
     uint32_t nl = 0, nd = 0;
     for (int L = 1; L < 16; L++) {
         nl += bcol[(kBColCntL + L) * 64];
         nd += bcol[(kBColCntD + L) * 64];
     }
-    if (nl > (uint32_t)kLaneLitCap || nd > (uint32_t)kLaneDistCap) return false;
+    if (nl > (uint32_t)C::kLit || nd > (uint32_t)C::kDist) {
+        if (over) *over = nl <= (uint32_t)kLaneLitCap && nd <= (uint32_t)kLaneDistCap;
+        return false;
+    }
     if (!lit.build(bcol + kBColCntL * 64) || !dist.build(bcol + kBColCntD * 64)) return false;
     {
         uint32_t ol = 0, od = 0;
@@ -404,7 +418,7 @@ __device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t 
         }
     }
     in.seek(lens_at);
-    lane_lengths(in, clc, nlit + ndist, nlit, col, bcol, 1, eob_ok);
+    lane_lengths<C>(in, clc, nlit + ndist, nlit, col, bcol, 1, eob_ok);
     in.seek(data_at);
     return true;
 }
@@ -493,7 +507,7 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
 #ifdef PMC_STAMPS
         uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (st == 0 && !lane_prepare(in, col, bcol, lit, dist, fixed)) st = 2;
+        if (st == 0 && !lane_prepare<LaneColsL>(in, col, bcol, lit, dist, fixed)) st = 2;
 #ifdef PMC_STAMPS
         uint64_t t1 = __builtin_amdgcn_s_memtime();
         uint64_t n_it = 0, n_act = 0;

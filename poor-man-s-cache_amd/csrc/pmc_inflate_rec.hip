@@ -35,13 +35,21 @@ namespace pmc {
 #define PMC_REC_STAGE 8
 #endif
 constexpr uint32_t kRecStage = PMC_REC_STAGE;         // staged records per lane (LDS column)
-constexpr uint32_t kRecFlushAt = kRecStage - 4;       // a lane this far behind makes the wave flush
-static_assert(kRecFlushAt + 3 < kRecStage && kRecStage % 4 == 0, "flushes leave < 4 records pending");
-static_assert((kRecStage & (kRecStage - 1)) == 0 && kRecFlushAt < kRecStage, "stage ring");
+constexpr uint32_t kRecFlushAt = 4;                   // a lane with a whole group makes the wave flush
+// (a flush leaves < 4 records pending, one step adds one: the ring never holds more than kRecFlushAt)
+static_assert(kRecFlushAt >= 4 && kRecFlushAt <= kRecStage && kRecStage % 4 == 0, "record stage ring");
+// lists of the record kernel: members of <= 4096 output bytes use distance codes 0..23 only (members
+// whose lists do not fit go to the lane kernel).  (88 lit/len entries and a 4-record stage fit 7
+// blocks per CU by bytes, but measured no faster than 6: LDS allocation granularity)
+#ifndef PMC_REC_LIT
+#define PMC_REC_LIT 96
+#endif
+typedef LaneCols<PMC_REC_LIT, 24> RecCols;
+static_assert((kRecStage & (kRecStage - 1)) == 0, "stage ring: a power of two");
 static_assert(kWinDw == 16, "the window prefetch holds one 8-dword half in two uint4");
 // phase A: code columns | input windows | record stage (the build columns live in the last
 // two, which start only after the tables are built)
-constexpr uint32_t kRecWinOff = (uint32_t)kColWords * 64 * 2;
+constexpr uint32_t kRecWinOff = (uint32_t)RecCols::kColWords * 64 * 2;
 constexpr uint32_t kRecStageOff = kRecWinOff + kWinDw * 64 * 4;
 constexpr uint32_t kRecLdsBytes = kRecStageOff + kRecStage * 64 * 4;
 static_assert((kBColCl + 19) * 64 <= (kWinDw + kRecStage) * 64 * 4, "build columns: window + stage");
@@ -140,7 +148,13 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
     const uint32_t rstride = a.rec_stride;
     PMC_GLB uint32_t *const rows = (PMC_GLB uint32_t *)a.rec_scratch + (uint64_t)blockIdx.x * 64 * rstride;
     PMC_GLB uint32_t *const row = rows + (uint64_t)lane * rstride;
-    for (uint64_t vb = (uint64_t)blockIdx.x * 64; vb < a.n; vb += (uint64_t)gridDim.x * 64) {
+    // 64-member batches from a work counter, the next grab in flight while a batch runs (a block
+    // that becomes resident late finds less work instead of adding a tail)
+    uint32_t nx = lane == 0 ? atomicAdd(a.rec_work, 1u) : 0u;
+    for (;;) {
+        const uint64_t vb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nx, 0) * 64;
+        if (vb >= a.n) break;
+        nx = lane == 0 ? atomicAdd(a.rec_work, 1u) : 0u;
         const uint64_t vi = vb + lane;
         const uint64_t v = a.order && vi < a.n ? (uint64_t)a.order[vi] : vi;
         const uint32_t in_len = v < a.n ? a.src_len[v] : 0u;
@@ -165,19 +179,20 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                 const uint32_t isz = in.byte_at(in_len - 4) | in.byte_at(in_len - 3) << 8 |
                                      in.byte_at(in_len - 2) << 16 | in.byte_at(in_len - 1) << 24;
                 if (isz > cap) st = 2;
-                else if (isz > kRecOutMax || isz > rstride) st = 4;
+                else if (isz > kRecOutMax) st = 4;
             }
         }
         LaneCode<15> lit, dist;
-        lit.base = (PMC_LDS int16_t *)(col + kColBaseL * 64);
-        lit.sym = col + kColLit * 64;
-        dist.base = (PMC_LDS int16_t *)(col + kColBaseD * 64);
-        dist.sym = col + kColDist * 64;
+        lit.base = (PMC_LDS int16_t *)(col + RecCols::kColBaseL * 64);
+        lit.sym = col + RecCols::kColLit * 64;
+        dist.base = (PMC_LDS int16_t *)(col + RecCols::kColBaseD * 64);
+        dist.sym = col + RecCols::kColDist * 64;
         bool fixed = false;
 #ifdef PMC_STAMPS
         uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (st == 0 && !lane_prepare(in, col, bcol, lit, dist, fixed)) st = 2;
+        bool over = false;
+        if (st == 0 && !lane_prepare<RecCols>(in, col, bcol, lit, dist, fixed, &over)) st = over ? 4u : 2u;
 #ifdef PMC_STAMPS
         uint64_t t1 = __builtin_amdgcn_s_memtime();
         uint64_t n_it = 0, n_act = 0;
@@ -247,8 +262,10 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                         olen = len;
                     }
                     if (st == 0) {
-                        if (pos + olen > ocap || nrec >= rstride) {
+                        if (pos + olen > ocap) {
                             st = 2;
+                        } else if (nrec >= rstride) { // more records than a row holds: the lane kernel's
+                            st = 4;
                         } else {
                             stg[(nrec & (kRecStage - 1)) * 64] = rec;
                             nrec++;

@@ -96,6 +96,7 @@ struct InflateArgs {
     uint32_t rec_stride;   // records per row (<= kRecMax)
     int32_t big_only;      // lane kernel: only members the record kernel marked kInflateBig
     int32_t stop_after;    // PMC_STAMPS / PMC_PHASE_STOP builds: record kernel ends after phase k
+    uint32_t *rec_work;    // record kernel: work counter (64-member batches handed out), zeroed per launch
 };
 
 // lane-inflate visit order: member indices grouped by compressed length, so a wave's 64
