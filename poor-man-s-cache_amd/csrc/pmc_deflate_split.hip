@@ -381,9 +381,10 @@ __global__ void __launch_bounds__(64) deflate_trees_kernel(DeflateArgs a) {
     PMC_LDS uint32_t *col = to_lds<uint32_t>(tl + l);
     PMC_LDS uint16_t *aux = to_lds<uint16_t>((uint16_t *)(tl + (CAP + 1) * 64) + l);
     if (CAP != kLCodes) {
-        // values in cO order: a wave's lanes get heaps of similar size and finish together
+        // values in cO order: a wave's lanes get heaps of similar size and finish together; the
+        // largest heaps first (blocks start in index order), so the kernel's last waves are short
         const uint64_t vi = (uint64_t)blockIdx.x * 64 + l;
-        if (vi < a.count) trees_value<CAP>(a, a.cO ? (uint64_t)a.cO[vi] : vi, vi, col, aux);
+        if (vi < a.count) trees_value<CAP>(a, a.cO ? (uint64_t)a.cO[a.count - 1 - vi] : vi, vi, col, aux);
     } else {
         const uint32_t nd = a.cD[a.count];
         for (uint32_t k = blockIdx.x * 64 + l; k < nd; k += gridDim.x * 64)

@@ -156,7 +156,8 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
         if (vb >= a.n) break;
         nx = lane == 0 ? atomicAdd(a.rec_work, 1u) : 0u;
         const uint64_t vi = vb + lane;
-        const uint64_t v = a.order && vi < a.n ? (uint64_t)a.order[vi] : vi;
+        // (longest members first: batches are handed out in order, so the kernel's last ones are short)
+        const uint64_t v = a.order && vi < a.n ? (uint64_t)a.order[a.n - 1 - vi] : vi;
         const uint32_t in_len = v < a.n ? a.src_len[v] : 0u;
         // st: 0 decoding, 1 end of block reached, 2 declined, 3 no member / empty input,
         // 4 output larger than the image (inflate_lane_kernel's)
