@@ -665,6 +665,9 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
                 rec_per_cu = nb;
             }
             const unsigned rb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * rec_per_cu);
+            // a batch that cannot fill the CUs once leaves phase B's member-serial wave loop exposed: there,
+            // members of more than 1 KiB output are faster in the lane kernel (all its work lane-parallel)
+            a.rec_max_out = (uint64_t)n >= (uint64_t)ctx->cus * rec_per_cu * 64 ? kRecOutMax : 1024u;
             r = ctx->recs.ensure((uint64_t)rb * 64 * rstride * 4 + 256);
             if (r) return r;
             a.rec_work = (uint32_t *)ctx->recs.p;

@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                 const uint32_t isz = in.byte_at(in_len - 4) | in.byte_at(in_len - 3) << 8 |
                                      in.byte_at(in_len - 2) << 16 | in.byte_at(in_len - 1) << 24;
                 if (isz > cap) st = 2;
-                else if (isz > kRecOutMax) st = 4;
+                else if (isz > a.rec_max_out) st = 4;
             }
         }
         LaneCode<15> lit, dist;

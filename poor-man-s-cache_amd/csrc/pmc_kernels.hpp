@@ -97,6 +97,7 @@ struct InflateArgs {
     int32_t big_only;      // lane kernel: only members the record kernel marked kInflateBig
     int32_t stop_after;    // PMC_STAMPS / PMC_PHASE_STOP builds: record kernel ends after phase k
     uint32_t *rec_work;    // record kernel: work counter (64-member batches handed out), zeroed per launch
+    uint32_t rec_max_out;  // record kernel: members of more output go to the lane kernel (<= kRecOutMax)
 };
 
 // lane-inflate visit order: member indices grouped by compressed length, so a wave's 64
