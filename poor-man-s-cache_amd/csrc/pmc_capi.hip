@@ -650,8 +650,10 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
         // members of <= kRecOutMax output bytes: the two-phase record kernel, one block per
         // resident wave (each block owns 64 record rows); larger ones: the lane kernel
         static const bool no_rec = getenv("PMC_INFLATE_REC") && !atoi(getenv("PMC_INFLATE_REC"));
+        // batches below this many members skip the record kernel (PMC_REC_MIN_N; default: none)
+        static const uint64_t rec_min_n = getenv("PMC_REC_MIN_N") ? strtoull(getenv("PMC_REC_MIN_N"), nullptr, 10) : 0;
         const unsigned lb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * 16);
-        if (!no_rec) {
+        if (!no_rec && (uint64_t)n >= rec_min_n) {
             const uint32_t rstride =
                 (uint32_t)std::min<uint64_t>(kRecMax, std::max<uint64_t>(64, ((uint64_t)max_len + 63) & ~(uint64_t)63));
             // exactly the resident blocks: a block owns its rows for the whole grid-stride loop,
