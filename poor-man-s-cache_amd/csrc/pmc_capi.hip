@@ -517,6 +517,10 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
             a.min_len = lo;
             a.lds_max_len = hi;
             a.cap_len = pcap;
+            // front work grabs: one value at 1 KiB and above, several for small values (whose parse is
+            // shorter than the counter's serialised grabs); PMC_FRONT_BATCH overrides
+            static const uint32_t fb_env = getenv("PMC_FRONT_BATCH") ? (uint32_t)atoi(getenv("PMC_FRONT_BATCH")) : 0u;
+            a.front_batch = fb_env ? std::min<uint32_t>(fb_env, 64u) : pcap <= 512 ? 4u : 1u;
             for (uint64_t first = 0; first < n; first += chunk) {
                 a.first = first;
                 a.count = std::min<uint64_t>(chunk, n - first);

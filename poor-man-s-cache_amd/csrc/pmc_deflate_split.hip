@@ -45,13 +45,11 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;
-    // Values come from a work counter, one at a time, the next one fetched while this one
-    // runs: value costs vary, and a static split left waves idle (a chunk of 555K values over
-    // 7168 resident waves is 1.2 rounds of 64-value groups).
-#ifndef PMC_FRONT_BATCH
-#define PMC_FRONT_BATCH 1
-#endif
-    constexpr uint32_t kBatch = PMC_FRONT_BATCH;
+    // Values come from a work counter, a.front_batch at a time, the next grab fetched while these
+    // run: value costs vary, and a static split left waves idle (a chunk of 555K values over 7168
+    // resident waves is 1.2 rounds of 64-value groups).  Grabs on one counter serialise in L2
+    // (~11 ns each): small values take several per grab, or the counter bounds the kernel.
+    const uint32_t kBatch = a.front_batch;
     uint32_t nx = l == 0 ? atomicAdd(a.cQ, kBatch) : 0u;
     for (;;) {
         const uint64_t g = readlane(nx, 0);

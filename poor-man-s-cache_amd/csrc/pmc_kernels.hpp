@@ -56,6 +56,7 @@ struct DeflateArgs {
     // whose rc is kDeflateRetry (a large-pass value of >= 16383 symbols: several DEFLATE blocks)
     uint64_t min_len;
     int32_t retry;
+    uint32_t front_batch; // split front: values per work-counter grab (>= 1)
 };
 
 constexpr int32_t kDeflateRetry = -7778;     // internal rc: the split pipeline declined the value
