@@ -522,3 +522,27 @@ def test_scattered_slots_in_place_store(ctx, D, golden):
     bk = back.cpu().numpy()
     bad = [k for k, (r, _) in enumerate(pairs) if bk[boff_h[k]:boff_h[k] + len(r)].tobytes() != r]
     assert not bad, bad[:10]
+
+
+def test_multi_megabyte_values_vs_oracle(ctx, D, golden):
+    """Values far past the split pipeline (the reference accepts values up to 512 MiB,
+    /root/reference/src/server/constants.hpp:8): 1 MiB of JSON slices, 2 MiB of a small binary alphabet,
+    4 MiB of a period-2 pattern, in one batch with small values; the reference's bytes and the round trip."""
+    from oracle import pyoracle as O
+    rng = np.random.default_rng(99)
+    corpus = golden.corpus * (1 + (1 << 20) // len(golden.corpus))
+    vals = [corpus[:1 << 20], bytes(rng.integers(0, 4, 2 << 20, dtype=np.uint8)), b"xy" * (2 << 20),
+            golden.corpus[:300], golden.corpus[5:1029]]
+    b = D.pack(vals)
+    out, rc = D.compress(ctx, b)
+    sync()
+    rc = rc.cpu().numpy()
+    got = out.host_items()
+    for k, v in enumerate(vals):
+        assert rc[k] == 0, (k, len(v), rc[k])
+        assert got[k] == O.compress(v), (k, len(v))
+    b2 = D.pack(got)
+    back, brc = D.decompress(ctx, b2, [len(v) for v in vals])
+    sync()
+    assert int((brc != 0).sum()) == 0
+    assert back.host_items() == vals
