@@ -800,7 +800,18 @@ struct SmallWave {
         uint64_t fast; // evaluated, usable, not cut, and position + 1 does not improve on it
         uint64_t impr; // evaluated, usable, not cut, < 258, and position + 1 improves on it
         uint64_t cut;  // evaluated, walk cut short (search() decides)
+#ifndef PMC_WALK_V1
+        // Step records (lane o): the outcome of a fresh-state walk entering the window at offset
+        // o, so a walk step is two v_readlane and one scalar branch instead of the mask shifts and
+        // find-first-sets of the stop / cut / impr / fast tests on the scalar unit.
+        //   w = type << 30 | pos << 24 | b   (FAST / PEND: pos = the match's offset t, b = its
+        //       length; CUT: pos = the stop; JUMP: b = the offset to continue from, 0..64)
+        //   t = (t - q) << 16 | b - 3       (the match token; q = its source)
+        uint32_t w, t;
+#endif
     };
+    static constexpr uint32_t kStepJump = 0, kStepCut = 1, kStepPend = 2, kStepFast = 3;
+    static constexpr uint32_t kNoWindow = 0x80000000u; // a p0 no position reaches (i - p0 >= 64)
     // 16 bytes at p as two 8-byte words (5 dword reads + alignbyte)
     __device__ void load16(uint32_t p, uint64_t &lo, uint64_t &hi) const {
         const uint32_t w = p >> 2, sh = p & 3;
@@ -921,6 +932,21 @@ struct SmallWave {
         g.fast = ballot((okfast & no_impr) != 0u);
         g.impr = ballot((okfast & impr) != 0u);
         g.cut = ballot((ev & cutc) != 0u);
+#ifndef PMC_WALK_V1
+        // step record of lane l (vector ALU; the masks are uniform): the first stop sj >= l, and
+        // from a usable sj the end st of its run of lazy improvements (impr bit 63 is clear)
+        const uint64_t sx = g.stop & (~0ull << l);
+        const uint32_t sj = sx ? (uint32_t)__builtin_ctzll(sx) : 64u, sjc = sj & 63u;
+        const uint32_t st = (uint32_t)__builtin_ctzll(~g.impr & (~0ull << sjc));
+        const uint32_t e0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(st << 2), (int)e);
+        const uint32_t b0 = e0 & 511u, q0 = (e0 >> 9) & 0x7fffu;
+        const uint32_t evs = (uint32_t)(g.m >> sjc) & (sj < 64 ? 1u : 0u), cts = (uint32_t)(g.cut >> sjc) & 1u;
+        const uint32_t fst = (uint32_t)(g.fast >> st) & 1u;
+        const uint32_t ty = evs ? (cts ? kStepCut : fst ? kStepFast : kStepPend) : kStepJump;
+        const uint32_t pos = cts ? sjc : st;
+        g.w = ty << 30 | pos << 24 | (evs ? b0 : sj);
+        g.t = (p0 + st - q0) << 16 | (b0 - 3u);
+#endif
     }
     // Token sink: tokens collect in one VGPR (lane k holds token 64 * block + k) and leave
     // with one coalesced store per 64 tokens, so emitting costs no exec-masked stores.
@@ -964,7 +990,20 @@ struct SmallWave {
     // [lf, len) goes out at the end -- no per-literal bookkeeping on the scalar unit.
     __device__ void tb_match(TokBuf &t, uint32_t lf, uint32_t s, uint32_t m) {
         const uint32_t l = (uint32_t)lane_id(), nl = s - lf, cnt = nl + 1;
-#ifndef PMC_DIAG_NOTOK
+#if !defined(PMC_DIAG_NOTOK) && !defined(PMC_WALK_V1)
+        // first 64 tokens with every lane storing (no exec mask work on the scalar unit): lanes
+        // past the run repeat the match token at its own slot, so no byte past it is written
+        {
+            const uint32_t k = l < nl ? l : nl;
+            tok[t.n + k] = k < nl ? lf + k : m;
+        }
+        if (cnt > 64) {
+            for (uint32_t b = 64; b < cnt; b += 64) {
+                const uint32_t k = b + l;
+                if (k < cnt) tok[t.n + k] = k < nl ? lf + k : m;
+            }
+        }
+#elif !defined(PMC_DIAG_NOTOK)
         for (uint32_t b = 0; b < cnt; b += 64) {
             const uint32_t k = b + l;
             if (k < cnt) tok[t.n + k] = k < nl ? lf + k : m;
@@ -1013,7 +1052,7 @@ struct SmallWave {
         stamp(11);
         PMC_STOP(13, 0)
         Group g;
-        g.p0 = 0xffffffffu;
+        g.p0 = kNoWindow;
         g.m = g.stop = g.fast = g.impr = g.cut = 0;
         g.e = 0;
         TokBuf tb;
@@ -1052,6 +1091,67 @@ struct SmallWave {
                          "v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
                          : "+v"(diag_v), "+v"(diag_v1), "+v"(diag_v2), "+v"(diag_v3));
 #endif
+#ifndef PMC_WALK_V1
+            if (ml == 2) {
+                // Fresh state.  Inside the current window the step record of offset i - p0 holds
+                // the whole step (positions without candidates are never stops, so no HC scan is
+                // needed there); otherwise jump to the next position with candidates and
+                // evaluate a window there.  Fast steps and jumps stay in this inner loop, whose
+                // few loop-carried values keep the scalar latch short; a pending lazy match or a
+                // cut walk leaves it for the general step.
+                uint32_t W = 0, off = 0;
+                for (;;) {
+                    off = i - g.p0;
+                    if (off >= 64) {
+                        uint32_t j = len;
+                        uint32_t w = i >> 6;
+                        if (w < nw) {
+                            if (w != hci) {
+                                hci = w;
+                                hcw = rfl64(HC[w]);
+                            }
+                            uint64_t m = hcw & (~0ull << (i & 63));
+                            while (!m && ++w < nw) {
+                                hci = w;
+                                hcw = rfl64(HC[w]);
+                                m = hcw;
+                            }
+                            if (m) j = w * 64 + (uint32_t)__builtin_ctzll(m);
+                        }
+                        i = j;
+                        if (i >= len) break;
+                        stamp(2);
+                        eval_group<PK>(g, i, npos, len);
+                        stamp(10);
+                        count(13);
+                        off = 0;
+                    }
+                    W = readlane(g.w, (int)off);
+                    const uint32_t ty = W >> 30;
+                    if (ty == kStepJump) { // no decision in this window from here: a new one at p0 + b
+                        i = g.p0 + (W & 127u);
+                        g.p0 = kNoWindow;
+                        continue;
+                    }
+                    if (ty != kStepFast) break;
+                    // literals up to the match at t, then the match
+                    const uint32_t t = g.p0 + ((W >> 24) & 63u);
+                    tb_match(tb, lf, t, readlane(g.t, (int)off));
+                    i = t + (W & 511u);
+                    lf = i;
+                    if (i >= len) break;
+                }
+                if (i >= len) break;
+                const uint32_t ps = g.p0 + ((W >> 24) & 63u);
+                if ((W >> 30) == kStepPend) { // t + 1 may improve on t's match (cut or unevaluated)
+                    i = ps + 1;
+                    ml = W & 511u;
+                    ms = ps - (readlane(g.t, (int)off) >> 16);
+                    continue;
+                }
+                i = ps; // a cut walk: the general step decides
+            }
+#else
             if (ml == 2) {
                 // no pending match: positions without chain candidates only pass the pending
                 // literal on, so jump to the next position that has candidates
@@ -1118,6 +1218,7 @@ struct SmallWave {
                     continue;
                 }
             }
+#endif
             count(9);
             const uint32_t pl = ml, pm = ms;
             ml = 2;
