@@ -804,10 +804,10 @@ struct SmallWave {
         // Step records (lane o): the outcome of a fresh-state walk entering the window at offset
         // o, so a walk step is two v_readlane and one scalar branch instead of the mask shifts and
         // find-first-sets of the stop / cut / impr / fast tests on the scalar unit.
-        //   w = type << 30 | pos << 24 | b   (FAST / PEND: pos = the match's offset t, b = its
-        //       length; CUT: pos = the stop; JUMP: b = the offset to continue from, 0..64)
-        //   t = (t - q) << 16 | b - 3       (the match token; q = its source)
-        uint32_t w, t;
+        //   w = type << 30 | pos << 24 | b   (FAST / PEND: pos = the match's offset t, whose
+        //       length and source the walk reads from e; CUT: pos = the stop; JUMP: b = the
+        //       offset to continue from, 0..64)
+        uint32_t w;
 #endif
     };
     static constexpr uint32_t kStepJump = 0, kStepCut = 1, kStepPend = 2, kStepFast = 3;
@@ -938,14 +938,11 @@ struct SmallWave {
         const uint64_t sx = g.stop & (~0ull << l);
         const uint32_t sj = sx ? (uint32_t)__builtin_ctzll(sx) : 64u, sjc = sj & 63u;
         const uint32_t st = (uint32_t)__builtin_ctzll(~g.impr & (~0ull << sjc));
-        const uint32_t e0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(st << 2), (int)e);
-        const uint32_t b0 = e0 & 511u, q0 = (e0 >> 9) & 0x7fffu;
         const uint32_t evs = (uint32_t)(g.m >> sjc) & (sj < 64 ? 1u : 0u), cts = (uint32_t)(g.cut >> sjc) & 1u;
         const uint32_t fst = (uint32_t)(g.fast >> st) & 1u;
         const uint32_t ty = evs ? (cts ? kStepCut : fst ? kStepFast : kStepPend) : kStepJump;
         const uint32_t pos = cts ? sjc : st;
-        g.w = ty << 30 | pos << 24 | (evs ? b0 : sj);
-        g.t = (p0 + st - q0) << 16 | (b0 - 3u);
+        g.w = ty << 30 | pos << 24 | sj;
 #endif
     }
     // Token sink: tokens collect in one VGPR (lane k holds token 64 * block + k) and leave
@@ -1135,9 +1132,10 @@ struct SmallWave {
                     }
                     if (ty != kStepFast) break;
                     // literals up to the match at t, then the match
-                    const uint32_t t = g.p0 + ((W >> 24) & 63u);
-                    tb_match(tb, lf, t, readlane(g.t, (int)off));
-                    i = t + (W & 511u);
+                    const uint32_t st = (W >> 24) & 63u, t = g.p0 + st, e0 = readlane(g.e, (int)st);
+                    const uint32_t b0 = e0 & 511u, q0 = (e0 >> 9) & 0x7fffu;
+                    tb_match(tb, lf, t, (t - q0) << 16 | (b0 - 3u));
+                    i = t + b0;
                     lf = i;
                     if (i >= len) break;
                 }
@@ -1145,8 +1143,9 @@ struct SmallWave {
                 const uint32_t ps = g.p0 + ((W >> 24) & 63u);
                 if ((W >> 30) == kStepPend) { // t + 1 may improve on t's match (cut or unevaluated)
                     i = ps + 1;
-                    ml = W & 511u;
-                    ms = ps - (readlane(g.t, (int)off) >> 16);
+                    const uint32_t e0 = readlane(g.e, (int)((W >> 24) & 63u));
+                    ml = e0 & 511u;
+                    ms = (e0 >> 9) & 0x7fffu;
                     continue;
                 }
                 i = ps; // a cut walk: the general step decides
