@@ -416,31 +416,62 @@ struct SmallWave {
         const uint32_t npos = rfl(npos_);
         const uint32_t l = (uint32_t)lane_id();
         PMC_LDS uint16_t *Tt = R;
+        // Both passes' digit counts in one pass over the positions (a histogram does not depend
+        // on the order): 256 u16 low-digit counters in tab (512 B), 128 u16 high-digit counters
+        // parked in S (untouched until the second scatter) and moved to tab after the first.
+        // Counted two per word by u32 LDS atomics.  (S holds the 256 B only from npos >= 128 on;
+        // shorter values count per pass.)
+        PMC_LDS uint32_t *hiw = (PMC_LDS uint32_t *)S;
+        const bool fused = npos >= 128;
+        auto scan_tab = [&]() { // 256 counters -> exclusive bases
+            const uint32_t t0 = tab[2 * l], t1 = tab[2 * l + 1];
+            const uint32_t v0 = t0 & 0xffffu, v1 = t0 >> 16, v2 = t1 & 0xffffu, v3 = t1 >> 16;
+            const uint32_t sum = v0 + v1 + v2 + v3;
+            const uint32_t b0 = wave_incl_scan_dpp(sum) - sum, b1 = b0 + v0, b2 = b1 + v1, b3 = b2 + v2;
+            tab[2 * l] = b0 | b1 << 16;
+            tab[2 * l + 1] = b2 | b3 << 16;
+        };
+        if (fused) {
+            for (uint32_t k = l; k < 128; k += 64) tab[k] = 0;
+            hiw[l] = 0;
+            wave_sync();
+            for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+                const uint32_t x = c0 + l;
+                const uint32_t h = hash3(load4(x < npos ? x : 0u));
+                if (x < npos) {
+                    lds_add(&tab[(h & 255) >> 1], 1u << (16 * (h & 1)));
+                    lds_add(&hiw[(h >> 9) & 63], 1u << (16 * ((h >> 8) & 1)));
+                }
+            }
+            wave_sync();
+            scan_tab();
+            const uint32_t u = hiw[l], u0 = u & 0xffffu, usum = u0 + (u >> 16);
+            const uint32_t c0 = wave_incl_scan_dpp(usum) - usum;
+            hiw[l] = c0 | (c0 + u0) << 16;
+            wave_sync();
+        }
         for (int pass = 0; pass < 2; pass++) {
             const uint32_t sh = pass ? 8 : 0;
             const int nb = pass ? 7 : 8;
             PMC_LDS uint16_t *dst = pass ? S : Tt;
-            // 256 u16 digit counters (512 B), counted two per word by u32 LDS atomics
             PMC_LDS uint16_t *tab16 = (PMC_LDS uint16_t *)tab;
-            for (uint32_t k = l; k < 128; k += 64) tab[k] = 0;
-            wave_sync();
-            for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
-                const uint32_t x = c0 + l;
-                const bool valid = x < npos;
-                const uint32_t p = valid ? (pass ? (uint32_t)Tt[x] : x) : 0u;
-                const uint32_t d = (hash3(load4(p)) >> sh) & 255;
-                if (valid) lds_add(&tab[d >> 1], 1u << (16 * (d & 1)));
+            if (fused && pass) { // the high-digit bases move out of S before the scatter writes it
+                tab[l] = hiw[l];
+                wave_sync();
+            } else if (!fused) { // 256 u16 digit counters (512 B) for this pass
+                for (uint32_t k = l; k < 128; k += 64) tab[k] = 0;
+                wave_sync();
+                for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+                    const uint32_t x = c0 + l;
+                    const bool valid = x < npos;
+                    const uint32_t p = valid ? (pass ? (uint32_t)Tt[x] : x) : 0u;
+                    const uint32_t d = (hash3(load4(p)) >> sh) & 255;
+                    if (valid) lds_add(&tab[d >> 1], 1u << (16 * (d & 1)));
+                }
+                wave_sync();
+                scan_tab();
+                wave_sync();
             }
-            wave_sync();
-            {
-                const uint32_t t0 = tab[2 * l], t1 = tab[2 * l + 1];
-                const uint32_t v0 = t0 & 0xffffu, v1 = t0 >> 16, v2 = t1 & 0xffffu, v3 = t1 >> 16;
-                const uint32_t sum = v0 + v1 + v2 + v3;
-                const uint32_t b0 = wave_incl_scan_dpp(sum) - sum, b1 = b0 + v0, b2 = b1 + v1, b3 = b2 + v2;
-                tab[2 * l] = b0 | b1 << 16;
-                tab[2 * l + 1] = b2 | b3 << 16;
-            }
-            wave_sync();
             for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
                 const uint32_t x = c0 + l;
                 const bool valid = x < npos;
