@@ -408,13 +408,17 @@ struct SmallWave {
     // beyond S, R and 1 KiB.  Within a 64-position chunk a lane's rank among the lanes holding
     // the same digit comes from one ballot per digit bit (match mask + mbcnt), so the scatter
     // is stable without per-lane counters.
-    __device__ __noinline__ void sort_positions2(uint32_t npos_, PMC_LDS uint32_t *tab) {
+    // Returns the rank of position 0 (the number of positions whose hash is smaller: the sort is
+    // stable and 0 is the lowest position); the rank array R itself is written by build_cn.
+    __device__ __noinline__ uint32_t sort_positions2(uint32_t npos_, PMC_LDS uint32_t *tab) {
         SmallWave me = *this; // (see parse_ondemand)
-        me.sort_positions2_body(npos_, tab);
+        return me.sort_positions2_body(npos_, tab);
     }
-    __device__ __forceinline__ void sort_positions2_body(uint32_t npos_, PMC_LDS uint32_t *tab) {
+    __device__ __forceinline__ uint32_t sort_positions2_body(uint32_t npos_, PMC_LDS uint32_t *tab) {
         const uint32_t npos = rfl(npos_);
         const uint32_t l = (uint32_t)lane_id();
+        const uint32_t h0 = rfl(hash3(load4(0)));
+        uint32_t k0 = 0;
         PMC_LDS uint16_t *Tt = R;
         // Both passes' digit counts in one pass over the positions (a histogram does not depend
         // on the order): 256 u16 low-digit counters in tab (512 B), 128 u16 high-digit counters
@@ -438,6 +442,7 @@ struct SmallWave {
             for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
                 const uint32_t x = c0 + l;
                 const uint32_t h = hash3(load4(x < npos ? x : 0u));
+                k0 += (uint32_t)__builtin_popcountll(ballot(x < npos && h < h0));
                 if (x < npos) {
                     lds_add(&tab[(h & 255) >> 1], 1u << (16 * (h & 1)));
                     lds_add(&hiw[(h >> 9) & 63], 1u << (16 * ((h >> 8) & 1)));
@@ -465,7 +470,8 @@ struct SmallWave {
                     const uint32_t x = c0 + l;
                     const bool valid = x < npos;
                     const uint32_t p = valid ? (pass ? (uint32_t)Tt[x] : x) : 0u;
-                    const uint32_t d = (hash3(load4(p)) >> sh) & 255;
+                    const uint32_t h = hash3(load4(p)), d = (h >> sh) & 255;
+                    if (!pass) k0 += (uint32_t)__builtin_popcountll(ballot(valid && h < h0));
                     if (valid) lds_add(&tab[d >> 1], 1u << (16 * (d & 1)));
                 }
                 wave_sync();
@@ -491,8 +497,7 @@ struct SmallWave {
             }
             wave_sync();
         }
-        for (uint32_t k = l; k < npos; k += 64) R[S[k]] = (uint16_t)k;
-        wave_sync();
+        return k0;
     }
 
     // 8 bytes at p (dword-aligned LDS reads + alignbyte; the value is zero padded)
@@ -784,10 +789,9 @@ struct SmallWave {
     // less position 0 (zlib's NIL: head[] value 0 never starts a match; the sort is stable,
     // so position 0 is the first entry of its run).  HC = CN > 0 as bits.
     template <int PK>
-    __device__ __forceinline__ void build_cn(uint32_t npos) {
+    __device__ __forceinline__ void build_cn(uint32_t npos, uint32_t k0) {
         constexpr uint32_t RB = 16 - (PK > 0 ? PK : 0), CMAX = PK > 0 ? (1u << PK) - 1 : 255u;
         const uint32_t l = (uint32_t)lane_id();
-        const uint32_t k0 = rfl((uint32_t)R[0]);
         if (PK < 0) { // has-candidate bits set by position below (HC as u32 words)
             for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
             wave_sync();
@@ -803,10 +807,10 @@ struct SmallWave {
             uint32_t rs = wave_incl_max_dpp(valid && h != hp ? k : 0u);
             rs = rs > prs ? rs : prs;
             const uint32_t cnt = k - rs - (rs == k0 && k > rs ? 1u : 0u);
-            if (valid) {
-                if (PK > 0) R[p] = (uint16_t)(k | (cnt < CMAX ? cnt : CMAX) << RB);
-                else if (PK == 0) CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
-                else if (cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
+            if (valid) { // (the rank array R is written here, not by the sort)
+                R[p] = (uint16_t)(PK > 0 ? k | (cnt < CMAX ? cnt : CMAX) << RB : k);
+                if (PK == 0) CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
+                else if (PK < 0 && cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
             }
             ph = readlane(h, 63);
             prs = readlane(rs, 63);
@@ -1063,9 +1067,10 @@ struct SmallWave {
     // (a noinline member reaches the wave state through `this`, a pointer to scratch: every
     // member pointer would be re-read from memory inside the loop.  A local copy lives in SGPRs.)
     template <int PK>
-    __device__ __noinline__ uint32_t parse_ondemand(uint32_t npos_, uint32_t len_) {
+    // (k0_: the rank of position 0, from sort_positions2; build_cn needs it before R exists)
+    __device__ __noinline__ uint32_t parse_ondemand(uint32_t npos_, uint32_t len_, uint32_t k0_) {
         SmallWave me = *this;
-        const uint32_t r = me.parse_ondemand_body<PK>(npos_, len_);
+        const uint32_t r = me.parse_ondemand_body<PK>(npos_, len_, k0_);
 #ifdef PMC_STAMPS
         for (int k = 0; k < 16; k++) st[k] = me.st[k];
         t_last = me.t_last;
@@ -1073,10 +1078,10 @@ struct SmallWave {
         return r;
     }
     template <int PK>
-    __device__ __forceinline__ uint32_t parse_ondemand_body(uint32_t npos_, uint32_t len_) {
+    __device__ __forceinline__ uint32_t parse_ondemand_body(uint32_t npos_, uint32_t len_, uint32_t k0_) {
         const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
         const uint32_t nw = (npos + 63) >> 6;
-        build_cn<PK>(npos);
+        build_cn<PK>(npos, rfl(k0_));
         stamp(11);
         PMC_STOP(13, 0)
         Group g;
@@ -2028,13 +2033,13 @@ struct SmallWave {
         const uint32_t npos = len >= 3 ? len - 2 : 0;
         uint32_t ntok;
         if (npos) {
-            sort_positions2(npos, (PMC_LDS uint32_t *)CN);
+            const uint32_t k0 = sort_positions2(npos, (PMC_LDS uint32_t *)CN);
             stamp(1);
             PMC_STOP(12, 0)
-            ntok = cnp == 6   ? parse_ondemand<6>(npos, len)
-                   : cnp == 4 ? parse_ondemand<4>(npos, len)
-                   : cnp < 0  ? parse_ondemand<-1>(npos, len)
-                              : parse_ondemand<0>(npos, len);
+            ntok = cnp == 6   ? parse_ondemand<6>(npos, len, k0)
+                   : cnp == 4 ? parse_ondemand<4>(npos, len, k0)
+                   : cnp < 0  ? parse_ondemand<-1>(npos, len, k0)
+                              : parse_ondemand<0>(npos, len, k0);
             PMC_STOP(14, 0)
         } else {
             lit_run(0, 0, len);
@@ -2118,7 +2123,7 @@ struct SmallWave {
         // (len - 3); literal = its position (dist 0), the byte is fetched in flush.
         uint32_t ntok;
         if (npos) {
-            ntok = parse_ondemand<false>(npos, len);
+            ntok = parse_ondemand<false>(npos, len, (uint32_t)R[0]);
         } else { // no position with MIN_MATCH lookahead: all literals
             lit_run(0, 0, len);
             ntok = len;
