@@ -792,10 +792,10 @@ struct SmallWave {
     __device__ __forceinline__ void build_cn(uint32_t npos, uint32_t k0) {
         constexpr uint32_t RB = 16 - (PK > 0 ? PK : 0), CMAX = PK > 0 ? (1u << PK) - 1 : 255u;
         const uint32_t l = (uint32_t)lane_id();
-        if (PK < 0) { // has-candidate bits set by position below (HC as u32 words)
-            for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
-            wave_sync();
-        }
+        // has-candidate bits set by position below (HC as u32 words, LDS atomics): no second
+        // pass over the positions
+        for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
+        wave_sync();
         uint32_t ph = 0xffffffffu, prs = 0; // previous chunk's last hash and run start
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
             const uint32_t k = c0 + l;
@@ -810,20 +810,12 @@ struct SmallWave {
             if (valid) { // (the rank array R is written here, not by the sort)
                 R[p] = (uint16_t)(PK > 0 ? k | (cnt < CMAX ? cnt : CMAX) << RB : k);
                 if (PK == 0) CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
-                else if (PK < 0 && cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
+                if (cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
             }
             ph = readlane(h, 63);
             prs = readlane(rs, 63);
         }
         wave_sync();
-        if (PK >= 0) {
-            for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
-                const uint32_t x = c0 + l;
-                const uint64_t m = ballot(x < npos && (PK > 0 ? ((uint32_t)R[x] >> RB) : (uint32_t)CN[x]) != 0);
-                if (l == 0) HC[c0 >> 6] = m;
-            }
-            wave_sync();
-        }
     }
     // results of the current eval: window start p0, evaluated offsets m (uniform) and, in
     // lane j, best | q << 9 | cut << 31 for position p0 + j
