@@ -275,7 +275,7 @@ uint64_t deflate_big_limit() {
     uint64_t lo = kSmallMax, hi = 32506;
     while (lo < hi) {
         uint64_t mid = (lo + hi + 1) / 2;
-        if (deflate_front_wave_bytes(mid) <= kLdsPerCu && deflate_back_wave_bytes(mid) + kCrcTabBytes <= kLdsPerCu)
+        if (deflate_front_wave_bytes(mid) <= kLdsPerCu && deflate_back_wave_bytes(mid) + kBackTabBytes <= kLdsPerCu)
             lo = mid;
         else
             hi = mid - 1;
@@ -490,7 +490,7 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
             const uint64_t fwb = deflate_front_wave_bytes(pcap), bwb = deflate_back_wave_bytes(pcap);
             Launch Lf = plan_lds(ctx, (const void *)deflate_front_kernel, fwb, n, front_crc ? kCrcTabBytes : 0);
             const size_t front_lds = Lf.lds - (front_crc ? kCrcTabBytes : 0);
-            Launch Lb = plan_lds(ctx, (const void *)deflate_back_kernel, bwb, n);
+            Launch Lb = plan_lds(ctx, (const void *)deflate_back_kernel, bwb, n, kBackTabBytes);
             const uint64_t chunk = chunk_of(pcap), blocks = chunk / 64;
             uint8_t *p = (uint8_t *)ctx->split.p;
             a.cT = (uint32_t *)p;

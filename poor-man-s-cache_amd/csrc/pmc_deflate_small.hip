@@ -2049,7 +2049,7 @@ struct SmallWave {
         const int l = lane_id();
         stage(src, len);
         PMC_STOP(21, 0)
-        const uint32_t crc = wave_crc32(b, len, crc_tab);
+        const uint32_t crc = wave_crc32_s8(bw, len, crc_tab); // (crc_tab: the back's slicing-by-8 tables)
         PMC_STOP(22, 0)
         for (uint64_t k = l; k < out_words; k += 64) outw[k] = 0;
         wave_sync();

@@ -395,11 +395,12 @@ template __global__ void deflate_trees_kernel<kLCodes>(DeflateArgs);
 // ---- back --------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    // slicing-by-8 CRC tables (8 KiB; table 0 is the plain byte table)
     uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
-    for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
+    for (int k = threadIdx.x; k < 8 * 256; k += blockDim.x) crc_tab[k] = c_crc_slice8[k];
     __syncthreads();
     const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
-    uint8_t *base = lds + 1024 + (uint64_t)wib * a.wave_bytes;
+    uint8_t *base = lds + kBackTabBytes + (uint64_t)wib * a.wave_bytes;
     const SmallLayout L = small_layout(a.cap_len);
     const BackLayout B = back_layout(a.cap_len);
     SmallWave w;

@@ -214,4 +214,68 @@ __device__ inline uint32_t wave_crc32(BytePtr buf, uint32_t len, TabPtr tab) {
     return ~acc;
 }
 
+// x^(8r) mod P for r < 16 (reflected domain: 0x80000000 is x^0; a multiply by x shifts right and
+// folds the polynomial in)
+struct CrcX8 {
+    uint32_t v[16];
+};
+constexpr CrcX8 make_crc_x8() {
+    CrcX8 t{};
+    uint32_t p = 0x80000000u;
+    for (int r = 0; r < 16; r++) {
+        t.v[r] = p;
+        for (int b = 0; b < 8; b++) p = (p >> 1) ^ ((p & 1u) ? kCrcPoly : 0u);
+    }
+    return t;
+}
+// xor over the wave, result uniform: row butterflies by DPP (quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror), then the four row totals.  All 64 lanes must be active.
+__device__ __forceinline__ uint32_t wave_xor_dpp(uint32_t v) {
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);
+    return readlane(v, 0) ^ readlane(v, 16) ^ readlane(v, 32) ^ readlane(v, 48);
+}
+// CRC-32 of buf[0..len) (bytes in LDS, read as words `bw`; the buffer may be read up to 4 bytes
+// past len) by the whole wave with slicing-by-8 (`s8`: c_crc_slice8 in LDS, 8 KiB).  16-byte
+// chunks aligned from the END as in wave_crc32, but every chunk starts from register 0 with zero
+// bytes in front of byte 0 (which leave a register-0 CRC unchanged), so a chunk is two table steps
+// of eight independent lookups instead of sixteen dependent ones; the init value's share
+// 0xFFFFFFFF x^(8 len) is added once.
+__device__ inline uint32_t wave_crc32_s8(PMC_LDS const uint32_t *bw, uint32_t len, PMC_LDS const uint32_t *s8) {
+    constexpr CrcX8 kX8 = make_crc_x8();
+    const uint32_t nchunks = (len + 15) >> 4;
+    uint32_t acc = 0;
+    for (uint32_t d = (uint32_t)lane_id(); d < nchunks; d += 64) {
+        const int32_t beg = (int32_t)len - 16 * (int32_t)(d + 1);
+        const int32_t wb = beg >> 2, lead = beg < 0 ? -beg : 0;
+        const uint32_t sh = (uint32_t)beg & 3u;
+        uint32_t w[5], x[4];
+#pragma unroll
+        for (int i = 0; i < 5; i++) w[i] = bw[wb + i > 0 ? wb + i : 0];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t v = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+            const int32_t r = lead - 4 * i;
+            x[i] = r <= 0 ? v : (r >= 4 ? 0u : v & (0xFFFFFFFFu << (8 * r)));
+        }
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const uint32_t a0 = x[2 * k] ^ c, a1 = x[2 * k + 1];
+            c = s8[7 * 256 + (a0 & 0xff)] ^ s8[6 * 256 + ((a0 >> 8) & 0xff)] ^ s8[5 * 256 + ((a0 >> 16) & 0xff)] ^
+                s8[4 * 256 + (a0 >> 24)] ^ s8[3 * 256 + (a1 & 0xff)] ^ s8[2 * 256 + ((a1 >> 8) & 0xff)] ^
+                s8[1 * 256 + ((a1 >> 16) & 0xff)] ^ s8[a1 >> 24];
+        }
+        acc ^= d ? multmodp(crc_shift_chunks(d), c) : c;
+    }
+    acc = wave_xor_dpp(acc);
+    if (len == 0) return 0;
+    const uint32_t ones = len <= kCrcQuarterMax ? c_crc_ones[len]
+                                                : multmodp(multmodp(crc_shift_chunks(len >> 4), kX8.v[len & 15]),
+                                                           0xFFFFFFFFu);
+    return ~(acc ^ ones);
+}
+
 } // namespace pmc

@@ -62,6 +62,7 @@ struct DeflateArgs {
 constexpr int32_t kDeflateRetry = -7778;     // internal rc: the split pipeline declined the value
 constexpr uint32_t kNtokMultiBlock = 0xffffffffu; // cN marker: >= 16383 symbols
 
+constexpr uint32_t kBackTabBytes = 8 * 256 * 4; // the back kernel's slicing-by-8 CRC tables (LDS per block)
 constexpr uint32_t kSplitRows = 336;  // 286 lit/len + 30 dist + 19 bit-length (+1)
 constexpr uint32_t kMergeRows = 572;  // 2 heap entries per merge, <= 285 merges
 constexpr uint32_t kPlanDeferred = 0xffffffffu;
