@@ -1882,12 +1882,20 @@ struct SmallWave {
             if (in && len && popc_lt(m) == 0) lds_add(&tmp[len], (uint32_t)__builtin_popcountll(m));
         }
         wave_sync();
-        if (l == 0) {
-            uint32_t code = 0;
-            for (int L = 1; L <= 15; L++) {
-                code = (code + (L > 1 ? tmp[L - 1] : 0u)) << 1;
-                tmp[16 + L] = code;
-            }
+        {
+            // next_code[L] = (next_code[L-1] + count[L-1]) << 1 unrolled: the sum over k < L of
+            // count[k] << (L - k) = (sum over k < L of count[k] << (16 - k)) >> (16 - L), exact
+            // since every term is a multiple of 2^(16 - L) -- one in-row DPP scan of lanes 1..15
+            // instead of fifteen dependent LDS round trips on one lane (count < 2^9: no overflow)
+            const uint32_t L = l & 15u, y = L ? tmp[L] << (16 - L) : 0u;
+            uint32_t v = y;
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+            const uint32_t nc = (v - y) >> (16 - L);
+            wave_sync();
+            if (l >= 1 && l < 16) tmp[16 + l] = nc;
         }
         wave_sync();
         for (int c0 = 0; c0 < elems; c0 += 64) {
@@ -1948,7 +1956,9 @@ struct SmallWave {
                 or_bits_lds(bitpos + 8, (uint32_t)(dcodes - 1), 5);
                 or_bits_lds(bitpos + 13, (uint32_t)(blcodes - 4), 4);
             }
-            if (l < blcodes) or_bits_lds(bitpos + 17 + 3 * l, blcode[TT.bl_order[l]] >> 16, 3);
+            // (bl_order in closed form: a per-lane index into __constant__ memory is a vector-memory
+            // round trip)
+            if (l < blcodes) or_bits_lds(bitpos + 17 + 3 * l, blcode[bl_order_cf(l)] >> 16, 3);
             bitpos += 17 + 3 * (uint64_t)blcodes;
             wave_sync();
             bitpos += send_runs(lcode, lcodes - 1, runL, bitpos);

@@ -467,7 +467,11 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
                 if (l == 0) a.rc[gv] = kDeflateRetry;
                 continue;
             }
-            for (uint32_t s = l; s < kSplitRows; s += 64) Ls[s] = a.cL[v * kSplitRows + s];
+            { // the code-length row (336 B; rows and Ls are 16-byte aligned) as dwords
+                PMC_GLB const uint32_t *row = (PMC_GLB const uint32_t *)(a.cL + v * kSplitRows);
+                PMC_LDS uint32_t *Lw = (PMC_LDS uint32_t *)Ls;
+                for (uint32_t k = l; k < kSplitRows / 4; k += 64) Lw[k] = row[k];
+            }
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
             const int rc = w.run_back(a.src + a.src_off[gv], len, ntok, plan, Ls, a.dst + a.dst_off[gv],
                                       a.dst_cap[gv], a.dst_len + gv);
