@@ -1874,12 +1874,21 @@ struct SmallWave {
             }
             return m;
         };
+        // pass 1: per-length counts; a group's first lane adds its group's size and gets back the
+        // count of the same length in earlier chunks (LDS atomics of one wave apply in order),
+        // which the group shares by ds_bpermute.  code_out[s] keeps that count + s's rank in the
+        // group until the next codes are known.
         for (int c0 = 0; c0 < elems; c0 += 64) {
             const int s = c0 + (int)l;
             const bool in = s < elems;
             const uint32_t len = in ? Ls[s] : 0u;
             const uint64_t m = group(len, in);
-            if (in && len && popc_lt(m) == 0) lds_add(&tmp[len], (uint32_t)__builtin_popcountll(m));
+            const uint32_t rank = popc_lt(m);
+            uint32_t prior = 0;
+            if (in && len && rank == 0) prior = lds_add(&tmp[len], (uint32_t)__builtin_popcountll(m));
+            const uint32_t lead = m ? (uint32_t)__builtin_ctzll(m) : l;
+            prior = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead << 2), (int)prior);
+            if (in) code_out[s] = prior + rank;
         }
         wave_sync();
         {
@@ -1898,18 +1907,15 @@ struct SmallWave {
             if (l >= 1 && l < 16) tmp[16 + l] = nc;
         }
         wave_sync();
+        // pass 2: code = next_code[len] + earlier same-length symbols (chunks independent)
         for (int c0 = 0; c0 < elems; c0 += 64) {
             const int s = c0 + (int)l;
-            const bool in = s < elems;
-            const uint32_t len = in ? Ls[s] : 0u;
-            const uint64_t m = group(len, in);
-            const uint32_t rank = popc_lt(m), mycode = len ? tmp[16 + len] + rank : 0u;
-            wave_sync();
-            const bool last = in && len && (m >> l) == 1; // highest lane of its group
-            if (last) tmp[16 + len] = mycode + 1;
-            if (in) code_out[s] = len ? ((__builtin_bitreverse32(mycode) >> (32 - len)) | (len << 16)) : 0u;
-            wave_sync();
+            if (s < elems) {
+                const uint32_t len = Ls[s], mycode = tmp[16 + len] + code_out[s];
+                code_out[s] = len ? ((__builtin_bitreverse32(mycode) >> (32 - len)) | (len << 16)) : 0u;
+            }
         }
+        wave_sync();
     }
     // the block as planned by deflate_trees_kernel: plan = type | l_max << 2 | d_max << 11 |
     // max_blindex << 16 (type 0 stored, 1 fixed, 2 dynamic); Ls = lit/len, dist, bl lengths
