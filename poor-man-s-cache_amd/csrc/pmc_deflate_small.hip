@@ -1618,6 +1618,51 @@ struct SmallWave {
         return base - pos;
     }
 
+    // scan_tree + send_tree in one go (the split back: the bl tree came from the trees kernel, so
+    // no counts): the run starts of all chunks first (one ballot each, kept in SGPRs), then each
+    // chunk's runs end at the next start, in the chunk or the first one after it -- no run-length
+    // array, no back-to-front pass, no second read of the neighbours.  NC = chunks at most.
+    template <int NC>
+    __device__ uint64_t send_runs_fused(PMC_LDS const uint32_t *code, int max_code, uint64_t pos) {
+        const int l = lane_id();
+        const int nch = max_code / 64 + 1;
+        uint64_t sm[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            sm[c] = 0;
+            if (c < nch) {
+                const int s = 64 * c + l;
+                const bool in = s <= max_code;
+                const uint32_t v = in ? code[s] >> 16 : 0xffffu;
+                const uint32_t vp = (in && s > 0) ? code[s - 1] >> 16 : 0xfffeu;
+                sm[c] = ballot(in && (s == 0 || v != vp));
+            }
+        }
+        uint32_t after[NC]; // first run start past chunk c (max_code + 1 if none)
+        uint32_t nxt = (uint32_t)max_code + 1;
+#pragma unroll
+        for (int c = NC - 1; c >= 0; c--) {
+            after[c] = nxt;
+            if (c < nch && sm[c]) nxt = 64u * c + (uint32_t)__builtin_ctzll(sm[c]);
+        }
+        uint64_t base = pos;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            if (c < nch) {
+                const int s = 64 * c + l;
+                const bool start = (sm[c] >> l) & 1;
+                const uint64_t above = l == 63 ? 0 : (sm[c] & (~0ull << (l + 1)));
+                const uint32_t e = above ? 64u * c + (uint32_t)__builtin_ctzll(above) : after[c];
+                const uint32_t v = start ? code[s] >> 16 : 0u, R = e - (uint32_t)s;
+                const uint32_t nb = start ? run_nbits(v, R) : 0u;
+                const uint32_t incl = wave_incl_scan_dpp(nb);
+                if (start) run_bits(v, R, base + incl - nb, true);
+                base += readlane(incl, 63);
+            }
+        }
+        return base - pos;
+    }
+
     // compress_block: every token's bits at its prefix-sum offset
     __device__ uint64_t emit_symbols(uint32_t ntok, uint64_t bitpos) {
         const int l = lane_id();
@@ -1951,10 +1996,6 @@ struct SmallWave {
             codes_from_lengths4(Ls + kLCodes, kDCodes, dcode, blfreq);
             codes_from_lengths4(Ls + kLCodes + kDCodes, kBLCodes, blcode, blfreq);
             PMC_STOP(23, bitpos)
-            PMC_LDS uint16_t *runL = runs, *runD = runs + 288;
-            scan_runs<false>(lcode, l_max, runL); // (the bl tree came from the trees kernel)
-            scan_runs<false>(dcode, d_max, runD);
-            wave_sync();
             const int lcodes = l_max + 1, dcodes = d_max + 1, blcodes = mbi + 1;
             if (l == 0) {
                 or_bits_lds(bitpos, (2u << 1) | 1u, 3);
@@ -1967,8 +2008,8 @@ struct SmallWave {
             if (l < blcodes) or_bits_lds(bitpos + 17 + 3 * l, blcode[bl_order_cf(l)] >> 16, 3);
             bitpos += 17 + 3 * (uint64_t)blcodes;
             wave_sync();
-            bitpos += send_runs(lcode, lcodes - 1, runL, bitpos);
-            bitpos += send_runs(dcode, dcodes - 1, runD, bitpos);
+            bitpos += send_runs_fused<(kLCodes + 63) / 64>(lcode, lcodes - 1, bitpos);
+            bitpos += send_runs_fused<1>(dcode, dcodes - 1, bitpos);
             wave_sync();
             PMC_STOP(24, bitpos)
         }
