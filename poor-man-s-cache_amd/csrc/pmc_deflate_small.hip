@@ -1962,6 +1962,58 @@ struct SmallWave {
         }
         wave_sync();
     }
+    // codes_from_lengths4 for the three trees at once (the split back's code-length row is
+    // contiguous: lit/len 286 | dist 30 | bl 19; the code slots lcode 288 | dcode 32 | blcode 32 are
+    // too): a group is (tree, length), 6 ballots; counts at tmp[tree * 16 + L], next codes at
+    // tmp[48 + tree * 16 + L] from one in-row DPP scan whose rows are the trees (96 words of tmp).
+    // One call and one set of passes instead of three.
+    __device__ __noinline__ void codes_from_lengths_all(PMC_LDS const uint8_t *Ls, PMC_LDS uint32_t *code0,
+                                                        PMC_LDS uint32_t *tmp) {
+        constexpr int E = kLCodes + kDCodes + kBLCodes;
+        const uint32_t l = (uint32_t)lane_id();
+        for (uint32_t k = l; k < 96; k += 64) tmp[k] = 0;
+        wave_sync();
+        auto tree_of = [](int s) { return s < kLCodes ? 0u : s < kLCodes + kDCodes ? 1u : 2u; };
+        for (int c0 = 0; c0 < E; c0 += 64) {
+            const int s = c0 + (int)l;
+            const bool in = s < E;
+            const uint32_t len = in ? Ls[s] : 0u, t = tree_of(s), key = t << 4 | len;
+            uint64_t m = ballot(in);
+#pragma unroll
+            for (int bt = 0; bt < 6; bt++) {
+                const uint64_t B = ballot((key >> bt) & 1);
+                m &= ((key >> bt) & 1) ? B : ~B;
+            }
+            const uint32_t rank = popc_lt(m);
+            uint32_t prior = 0;
+            if (in && len && rank == 0) prior = lds_add(&tmp[key], (uint32_t)__builtin_popcountll(m));
+            const uint32_t lead = m ? (uint32_t)__builtin_ctzll(m) : l;
+            prior = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead << 2), (int)prior);
+            if (in) code0[s + 2 * t] = prior + rank; // (slots: s, 288 + s - 286, 320 + s - 316)
+        }
+        wave_sync();
+        {
+            const uint32_t L = l & 15u, y = (L && l < 48) ? tmp[l] << (16 - L) : 0u;
+            uint32_t v = y;
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+            v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+            const uint32_t nc = (v - y) >> (16 - L);
+            wave_sync();
+            if (l < 48 && L >= 1) tmp[48 + l] = nc;
+        }
+        wave_sync();
+        for (int c0 = 0; c0 < E; c0 += 64) {
+            const int s = c0 + (int)l;
+            if (s < E) {
+                const uint32_t len = Ls[s], t = tree_of(s), slot = (uint32_t)s + 2 * t;
+                const uint32_t mycode = tmp[48 + (t << 4 | len)] + code0[slot];
+                code0[slot] = len ? ((__builtin_bitreverse32(mycode) >> (32 - len)) | (len << 16)) : 0u;
+            }
+        }
+        wave_sync();
+    }
     // the block as planned by deflate_trees_kernel: plan = type | l_max << 2 | d_max << 11 |
     // max_blindex << 16 (type 0 stored, 1 fixed, 2 dynamic); Ls = lit/len, dist, bl lengths
     __device__ uint64_t emit_planned(uint32_t ntok, uint32_t len, uint64_t bitpos, uint32_t plan,
@@ -1992,9 +2044,8 @@ struct SmallWave {
             wave_sync();
         } else {
             const int l_max = (int)((plan >> 2) & 511), d_max = (int)((plan >> 11) & 31), mbi = (int)((plan >> 16) & 31);
-            codes_from_lengths4(Ls, kLCodes, lcode, blfreq); // (blfreq: free scratch in the back)
-            codes_from_lengths4(Ls + kLCodes, kDCodes, dcode, blfreq);
-            codes_from_lengths4(Ls + kLCodes + kDCodes, kBLCodes, blcode, blfreq);
+            // (lcode | dcode | blcode contiguous; runs is free scratch in the split back)
+            codes_from_lengths_all(Ls, lcode, (PMC_LDS uint32_t *)runs);
             PMC_STOP(23, bitpos)
             const int lcodes = l_max + 1, dcodes = d_max + 1, blcodes = mbi + 1;
             if (l == 0) {
