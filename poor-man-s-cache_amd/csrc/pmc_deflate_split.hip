@@ -428,6 +428,10 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
         const bool in = (uint32_t)l < kBatch && vl < a.count;
         const uint32_t myl = in ? a.src_len[a.first + vl] : 0u;
         const uint32_t myn = in ? a.cN[vl] : 0u, myp = in ? a.cP[vl] : 0u;
+        // (source / destination offsets and capacities of the batch load with its lengths: no
+        // dependent round trip per value for its addresses)
+        const uint64_t myo = in ? a.src_off[a.first + vl] : 0u, mydo = in ? a.dst_off[a.first + vl] : 0u;
+        const uint32_t myc = in ? a.dst_cap[a.first + vl] : 0u;
         // (the small pass, min_len 0, also answers empty values: rc = INVALID_INPUT below)
         uint64_t todo = ballot(in && (a.min_len == 0 || myl > a.min_len) && myl <= a.lds_max_len);
         while (todo) {
@@ -442,9 +446,9 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
             uint32_t pf = 0;
             if (todo) {
                 const int j2 = __builtin_ctzll(todo);
-                const uint64_t v2 = g + (uint64_t)j2, gv2 = a.first + v2;
+                const uint64_t v2 = g + (uint64_t)j2;
                 const uint32_t len2 = readlane(myl, j2), n2 = readlane(myn, j2);
-                const uintptr_t sa = (uintptr_t)(a.src + a.src_off[gv2]), ta = (uintptr_t)(a.cT + v2 * a.cap_len),
+                const uintptr_t sa = (uintptr_t)(a.src + readlane64(myo, j2)), ta = (uintptr_t)(a.cT + v2 * a.cap_len),
                                 la = (uintptr_t)(a.cL + v2 * kSplitRows);
                 const uint32_t ns = (uint32_t)(((sa & 127) + len2 + 127) >> 7),
                                nt = n2 == kNtokMultiBlock ? 0u : (uint32_t)(((ta & 127) + 4ull * n2 + 127) >> 7),
@@ -473,8 +477,8 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
                 for (uint32_t k = l; k < kSplitRows / 4; k += 64) Lw[k] = row[k];
             }
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
-            const int rc = w.run_back(a.src + a.src_off[gv], len, ntok, plan, Ls, a.dst + a.dst_off[gv],
-                                      a.dst_cap[gv], a.dst_len + gv);
+            const int rc = w.run_back(a.src + readlane64(myo, j), len, ntok, plan, Ls, a.dst + readlane64(mydo, j),
+                                      readlane(myc, j), a.dst_len + gv);
             if (l == 0) {
                 a.rc[gv] = rc;
                 if (rc) a.dst_len[gv] = 0;

@@ -161,6 +161,9 @@ __device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
 __device__ __forceinline__ uint32_t readlane(uint32_t v, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return (uint64_t)readlane((uint32_t)(v >> 32), l) << 32 | readlane((uint32_t)v, l);
+}
 // v_writelane without inline asm: compare + select (2 VALU, no hazards to pad)
 __device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t v, int l) {
     return lane_id() == l ? v : old;
