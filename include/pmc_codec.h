@@ -31,7 +31,7 @@ extern "C" {
 #define PMC_Z_MEM_ERROR (-4)     /* device allocation failed                               */
 #define PMC_Z_BUF_ERROR (-5)     /* truncated stream (reference hangs here)     */
 #define PMC_E_NO_DEVICE (-100)   /* no usable gfx950 device / HIP runtime error            */
-#define PMC_E_CAPACITY (-101)    /* output capacity too small (batched API only)           */
+#define PMC_E_CAPACITY (-101)    /* output capacity too small; decompress: dst_len = needed  */
 #define PMC_E_ARG (-102)         /* invalid argument                                       */
 
 /* One device + streams + scratch.  The host-memory calls (single value, *_batch_host,
@@ -56,8 +56,13 @@ size_t pmc_gzip_bound(size_t len);
 /* ---- single value, host memory (what GzipCompressor::Compress/Decompress wrap) ----
  * pmc_gzip_compress: compress in[0..in_len) into out (capacity out_cap >= pmc_gzip_bound).
  *   in_len == 0 or in == NULL -> PMC_INVALID_INPUT (gzip_compressor.cpp:4).
- * pmc_gzip_decompress: decompress one gzip member; *out_len receives the size.  The
- *   caller sizes `out` from pmc_gzip_isize(); PMC_E_CAPACITY if the stream is longer. */
+ * pmc_gzip_decompress: decompress the first gzip member of in[0..in_len) (bytes after its
+ *   trailer are ignored, as the reference's inflate loop stops at Z_STREAM_END,
+ *   gzip_compressor.cpp:96); *out_len receives the size.  The caller sizes `out` from
+ *   pmc_gzip_isize() (the last 4 bytes: right unless bytes follow the member).  If the stream
+ *   decodes past out_cap the call returns PMC_E_CAPACITY with *out_len = the decoded size and
+ *   no verdict yet: call again with that much room (the reference grows its buffer instead,
+ *   :71-77, so capacity is never one of its verdicts). */
 int pmc_gzip_compress(pmc_ctx *ctx, const void *in, size_t in_len, void *out, size_t out_cap,
                       size_t *out_len);
 int pmc_gzip_decompress(pmc_ctx *ctx, const void *in, size_t in_len, void *out, size_t out_cap,
@@ -80,8 +85,11 @@ uint32_t pmc_gzip_isize(const void *in, size_t in_len);
  * decompress call of one context may run concurrently on two streams.
  * Compress: src_len[i] == 0 -> rc PMC_INVALID_INPUT (reference semantics).  Input bytes
  *   may contain NULs (binary safe; the single-value drop-in keeps the reference's strlen).
- * Decompress: dst_cap[i] must be >= the decompressed size (ISIZE); use
- *   pmc_gzip_isize_batch to read the trailers on device. */
+ * Decompress: dst_cap[i] should be >= the decompressed size (ISIZE); use
+ *   pmc_gzip_isize_batch to read the trailers on device.  Bytes after a member's trailer are
+ *   ignored (gzip_compressor.cpp:96).  A member that decodes past dst_cap[i] gets
+ *   rc[i] = PMC_E_CAPACITY and dst_len[i] = its decoded size (no verdict yet; decode it again
+ *   with that capacity). */
 int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
                             const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
                             const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
@@ -146,8 +154,9 @@ int pmc_gzip_decompress_batch_pinned(pmc_ctx *ctx, const uint8_t *src, const uin
  * Entry.value of a compressed entry (/root/reference/src/kvs/kvs.hpp:38-44, filled at
  * kvs.cpp:185-187) becomes a pmc_extent, an extent of one device heap.  The caller keeps its own
  * key index (the reference's hash table stays on the host) and stores the extent in it.
- *   put: values (host memory) -> pinned staging -> H2D -> compress straight into freshly
- *        allocated extents (gzip_bound(len) rounded to 16 B) -> only lengths come back.
+ *   put: values (host memory) -> pinned staging -> H2D -> compress into the put's device staging
+ *        -> lengths come back -> extents of the MEMBER's size (rounded to 16 B) are allocated and
+ *        the members compacted into them on the device: the heap holds ~C bytes per value.
  *   get: extents -> decompress on the device into a packed response image, optionally framed
  *        as the server's wire format (f3: the custom protocol's value + 0x1F, or a RESP bulk
  *        string "$<len>\r\n<value>\r\n", /root/reference/src/server/protocol.cpp:399-406,
@@ -173,7 +182,8 @@ int pmc_store_create(pmc_ctx *ctx, uint64_t heap_bytes, pmc_store **out);
 void pmc_store_destroy(pmc_store *s);
 /* Compress value i (src + src_off[i], src_len[i] bytes, host memory) into a new extent:
  * ext[i] (flags 1) and rc[i] = 0, or rc[i] = PMC_Z_MEM_ERROR (heap full) / a codec code with
- * ext[i].flags = 0.  Returns PMC_OK unless the call itself failed. */
+ * ext[i].flags = 0.  Returns PMC_OK unless the call itself failed; then every value's rc[i] holds
+ * the failure, ext[i].flags = 0 and no extent stays allocated. */
 int pmc_store_put_batch(pmc_store *s, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
                         uint32_t n, pmc_extent *ext, int32_t *rc);
 /* Decompress extents into framed responses (frame = PMC_FRAME_*): resp[i], resp_len[i], rc[i]. */

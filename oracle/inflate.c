@@ -270,7 +270,10 @@ int oracle_gzip_decompress(const uint8_t *in, size_t in_len, uint8_t *out, size_
     p = (size_t)(s->bitpos >> 3);
     if (in_len < p + 4) return Z_BUF_ERROR;
     uint32_t crc = in[p] | ((uint32_t)in[p + 1] << 8) | ((uint32_t)in[p + 2] << 16) | ((uint32_t)in[p + 3] << 24);
-    if (s->out_n > s->out_cap) return Z_DATA_ERROR; /* cannot have matched ISIZE-sized cap */
+    if (s->out_n > s->out_cap) { /* decoded past the buffer: report the size, no verdict yet */
+        *out_len = s->out_n;
+        return ORACLE_E_CAPACITY;
+    }
     if (crc != oracle_crc32(0, out, s->out_n)) return Z_DATA_ERROR;
     p += 4;
     if (in_len < p + 4) return Z_BUF_ERROR;

@@ -43,7 +43,12 @@ size_t oracle_gzip_compress_dp(const uint8_t *in, size_t len, uint8_t *out);
 /* gzip-only inflate with zlib 1.2.11 inflateInit2(31) validation rules.
  * Returns 0 (Z_STREAM_END reached), -3 (Z_DATA_ERROR) or -5 (Z_BUF_ERROR: truncated
  * input -- the reference loops forever here; this is the documented
- * divergence).  Output beyond out_cap is counted but not stored. */
+ * divergence), or ORACLE_E_CAPACITY (-101) when the stream decodes past out_cap: output beyond
+ * out_cap is counted but not stored, *out_len receives the decoded size and the caller retries
+ * with that capacity (the reference grows its buffer instead, gzip_compressor.cpp:71-77, so
+ * capacity is never a verdict).  Bytes after the first member's trailer are ignored
+ * (gzip_compressor.cpp:96 stops at Z_STREAM_END). */
+#define ORACLE_E_CAPACITY (-101)
 int oracle_gzip_decompress(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_cap,
                            size_t *out_len);
 

@@ -68,14 +68,24 @@ def isize(gz: bytes) -> int:
     return int.from_bytes(gz[-4:], "little") if len(gz) >= 4 else 0
 
 
-def decompress(gz: bytes, cap=None):
-    """Returns (rc, bytes).  rc: 0, -3 (Z_DATA_ERROR), -5 (truncated)."""
+CAPACITY = -101  # ORACLE_E_CAPACITY: decoded past the buffer (never a verdict of the reference)
+
+
+def decompress(gz: bytes, cap=None, grow=True):
+    """Returns (rc, bytes).  rc: 0, -3 (Z_DATA_ERROR), -5 (truncated).  The first capacity guess
+    is the ISIZE trailer (last 4 bytes); a stream that decodes past it is retried with the decoded
+    size, as the reference's doubling buffer would hold it (gzip_compressor.cpp:71-77).  With
+    grow=False a capacity overflow returns (CAPACITY, b"")."""
     L = lib()
     if cap is None:
-        cap = max(isize(gz), 1) + 64
-    out = ctypes.create_string_buffer(cap)
-    n = ctypes.c_size_t(0)
-    rc = L.oracle_gzip_decompress(gz, len(gz), out, cap, ctypes.byref(n))
+        cap = min(max(isize(gz), 1) + 64, 1032 * len(gz) + 64)
+    for _ in range(2):
+        out = ctypes.create_string_buffer(max(cap, 1))
+        n = ctypes.c_size_t(0)
+        rc = L.oracle_gzip_decompress(gz, len(gz), out, cap, ctypes.byref(n))
+        if rc != CAPACITY or not grow:
+            break
+        cap = n.value
     return rc, (out.raw[:n.value] if rc == 0 else b"")
 
 

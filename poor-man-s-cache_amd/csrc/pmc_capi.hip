@@ -182,6 +182,12 @@ struct pmc_ctx {
     };
     std::vector<KRec> krecs;
     std::mutex host_mu;          // host-API calls (host_batch, pinned_batch) of this context, one at a time
+    // per direction: the scratch buffers above (DevBuf::ensure may free and reallocate them) and
+    // dir_ev / dir_st / dir_used are touched by one enqueueing thread at a time, whichever API
+    // (device batch, host batch, pinned, store, slab) it came through; a compress and a decompress
+    // still enqueue concurrently.  Recursive: the slab and store calls hold it around their own
+    // dir_enter / dir_leave and call the batch entry points inside.
+    std::recursive_mutex dir_mu[2];
     DevBuf staging;              // device side of host-API calls
     uint64_t *dbg = nullptr;     // diagnostic stamp sums (PMC_STAMPS builds)
     HostBuf pinned;              // host side of host-API calls
@@ -744,6 +750,7 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
     hipStream_t st = (hipStream_t)stream;
+    std::lock_guard<std::recursive_mutex> dir_lock(ctx->dir_mu[0]);
     int r = dir_enter(ctx, 0, st);
     if (r) return r;
     r = compress_batch_body(ctx, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len, stream);
@@ -758,6 +765,7 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
     hipStream_t st = (hipStream_t)stream;
+    std::lock_guard<std::recursive_mutex> dir_lock(ctx->dir_mu[1]);
     int r = dir_enter(ctx, 1, st);
     if (r) return r;
     r = decompress_batch_body(ctx, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len, stream);

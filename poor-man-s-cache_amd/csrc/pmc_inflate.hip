@@ -494,7 +494,10 @@ struct InflateWave {
         // 3. trailer: CRC-32 then ISIZE (inflate.c CHECK / LENGTH)
         uint64_t tp = (br.pos + 7) >> 3;
         if (in_len < tp + 4) return PMC_Z_BUF_ERROR_DEV;
-        if (outn > cap) return PMC_Z_DATA_ERROR_DEV;
+        if (outn > cap) { // a valid stream so far that needs more room: report the size (no verdict yet)
+            if (l == 0) *dst_len = outn > 0xffffffffull ? 0xffffffffu : (uint32_t)outn;
+            return PMC_E_CAPACITY_DEV;
+        }
         sync();
         uint32_t crc = wave_crc32(out, (uint32_t)outn, crc_tab);
         uint32_t want = inb[tp] | ((uint32_t)inb[tp + 1] << 8) | ((uint32_t)inb[tp + 2] << 16) | ((uint32_t)inb[tp + 3] << 24);
@@ -1053,7 +1056,10 @@ struct InflateLds {
         // 3. trailer: CRC-32 then ISIZE (inflate.c CHECK / LENGTH)
         const uint32_t tp = (sb.pos() + 7) >> 3;
         if (in_len < tp + 4) return PMC_Z_BUF_ERROR_DEV;
-        if (o > cap) return PMC_Z_DATA_ERROR_DEV;
+        if (o > cap) { // a valid stream so far that needs more room: report the size (no verdict yet)
+            if (l == 0) *dst_len = o;
+            return PMC_E_CAPACITY_DEV;
+        }
         const uint32_t crc = wave_crc32(out, o, crc_tab);
         const uint32_t want = inb[tp] | ((uint32_t)inb[tp + 1] << 8) | ((uint32_t)inb[tp + 2] << 16) |
                               ((uint32_t)inb[tp + 3] << 24);
@@ -1147,7 +1153,7 @@ __global__ void __launch_bounds__(256, 5) inflate_kernel(InflateArgs a) {
             }
             if (l == 0) {
                 a.rc[v] = rc;
-                if (rc) a.dst_len[v] = 0;
+                if (rc && rc != PMC_E_CAPACITY_DEV) a.dst_len[v] = 0;
             }
         }
     }

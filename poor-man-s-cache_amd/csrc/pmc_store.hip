@@ -10,8 +10,9 @@
 //     which crosses PCIe once into a pinned buffer; the wire framing (custom protocol's 0x1F or a
 //     RESP bulk string header/trailer) is written around each value in that buffer, so the value
 //     bytes are never copied on the host (f3).
-// The heap allocator is host-side: extents of gzip_bound(len) rounded to 16 B (to 1/8 of a power of
-// two above 8 KiB), per-size free lists, bump allocation otherwise.  Compiled into the unity TU after
+// The heap allocator is host-side: extents of the member's compressed length rounded to 16 B (to 1/8
+// of a power of two above 8 KiB), per-size free lists, bump allocation otherwise.  A put compresses
+// into gzip_bound slots of its device staging, learns the lengths, allocates, then compacts.  Compiled into the unity TU after
 // pmc_capi.hip (uses pmc_ctx, DevBuf, HostBuf, the scan/compact kernels).
 
 #include <unordered_map>
@@ -34,8 +35,10 @@ struct pmc_store {
 
 namespace {
 
+// bytes reserved for a member of `len` bytes: 16-byte granules, and above 8 KiB steps of 1/8 of
+// the power of two below (bounded waste, few distinct free-list sizes)
 uint32_t extent_size(uint64_t len) {
-    uint64_t c = (gzip_bound(len) + 15) & ~(uint64_t)15;
+    uint64_t c = (len + 15) & ~(uint64_t)15;
     if (c > 8192) {
         uint64_t p = 1;
         while (p * 2 <= c) p *= 2;
@@ -128,84 +131,110 @@ PMC_API int pmc_store_put_batch(pmc_store *s, const uint8_t *src, const uint64_t
     if (n == 0) return PMC_OK;
     StoreCall call(s, s->put_mu);
     pmc_ctx *ctx = s->ctx;
-    // values sent to the codec: non-empty ones that got an extent
+    // values sent to the codec: the non-empty ones.  They are compressed into gzip_bound slots of the
+    // put's device staging first; extents are allocated only once the compressed lengths are known,
+    // so the heap holds ~C bytes per value, not the uncompressed bound (kvs.hpp:38-44 keeps C bytes).
     std::vector<uint32_t> pick;
     pick.reserve(n);
-    uint64_t bytes = 0, max_len = 1;
-    std::unique_lock<std::mutex> alloc(s->alloc_mu);
+    uint64_t bytes = 0, slots = 0, max_len = 1;
     for (uint32_t i = 0; i < n; i++) {
         ext[i] = pmc_extent{0, 0, 0, 0, 0};
         if (src_len[i] == 0) {
             rc[i] = PMC_INVALID_INPUT;
             continue;
         }
-        const uint32_t size = extent_size(src_len[i]);
-        uint64_t off = 0;
-        if (!store_alloc(s, size, &off)) {
-            rc[i] = PMC_Z_MEM_ERROR;
-            continue;
-        }
-        ext[i] = pmc_extent{off, size, 0, src_len[i], 1};
         rc[i] = PMC_OK;
         pick.push_back(i);
         bytes += src_len[i];
+        slots += (gzip_bound(src_len[i]) + 15) & ~(uint64_t)15;
         max_len = std::max<uint64_t>(max_len, src_len[i]);
     }
-    alloc.unlock();
     const uint32_t m = (uint32_t)pick.size();
     if (m == 0) return PMC_OK;
-    // staging: soff | doff (u64) | slen | dcap | dlen | rc (u32) | value bytes
-    const uint64_t meta = al256(m * 8ull) * 2 + al256(m * 4ull) * 4;
-    int r = s->phost.ensure(meta + bytes + 64);
-    if (!r) r = s->pdev.ensure(meta + bytes + 64);
-    if (r) {
-        std::lock_guard<std::mutex> a(s->alloc_mu);
-        for (uint32_t k = 0; k < m; k++) {
-            store_release(s, ext[pick[k]]);
-            rc[pick[k]] = r;
-        }
-        return r;
-    }
+    auto fail_all = [&](int code) {  // nothing was allocated yet
+        for (uint32_t k = 0; k < m; k++) rc[pick[k]] = code;
+        return code;
+    };
+    // staging: soff | doff | poff (u64) | slen | dcap | dlen | rc (u32) | value bytes | member slots
+    const uint64_t meta = al256(m * 8ull) * 3 + al256(m * 4ull) * 4;
+    const uint64_t vb = al256(bytes + 16);
+    int r = s->phost.ensure(meta + vb);
+    if (!r) r = s->pdev.ensure(meta + vb + slots + 64);
+    if (r) return fail_all(r);
     uint8_t *hp = (uint8_t *)s->phost.p, *dp = (uint8_t *)s->pdev.p;
     uint64_t *h_soff = (uint64_t *)hp, *h_doff = (uint64_t *)(hp + al256(m * 8ull));
-    uint32_t *h_slen = (uint32_t *)(hp + al256(m * 8ull) * 2);
+    uint64_t *h_poff = (uint64_t *)(hp + al256(m * 8ull) * 2);
+    uint32_t *h_slen = (uint32_t *)(hp + al256(m * 8ull) * 3);
     uint32_t *h_dcap = (uint32_t *)((uint8_t *)h_slen + al256(m * 4ull));
     uint32_t *h_dlen = (uint32_t *)((uint8_t *)h_dcap + al256(m * 4ull));
     int32_t *h_rc = (int32_t *)((uint8_t *)h_dlen + al256(m * 4ull));
     uint8_t *h_src = hp + meta;
+    uint8_t *d_slots = dp + meta + vb;
     const uint64_t d_base = (uint64_t)(dp - hp);  // device address = host address + d_base
     auto dev = [&](void *h) { return (uint8_t *)h + d_base; };
-    uint64_t so = 0;
+    uint64_t so = 0, doff = 0;
     for (uint32_t k = 0; k < m; k++) {
         const uint32_t i = pick[k];
         h_soff[k] = so;
         h_slen[k] = src_len[i];
         memcpy(h_src + so, src + src_off[i], src_len[i]);
         so += src_len[i];
-        h_doff[k] = ext[i].off;
-        h_dcap[k] = ext[i].cap;
+        h_doff[k] = doff;
+        h_dcap[k] = (uint32_t)gzip_bound(src_len[i]);
+        doff += (gzip_bound(src_len[i]) + 15) & ~(uint64_t)15;
     }
     hipStream_t st = ctx->stream;
-    HIP_TRY(hipMemcpyAsync(dp, hp, meta + bytes, hipMemcpyHostToDevice, st));
-    r = pmc_gzip_compress_batch(ctx, dev(h_src), (uint64_t *)dev(h_soff), (uint32_t *)dev(h_slen), m,
-                                (uint8_t *)s->heap.p, (uint64_t *)dev(h_doff), (uint32_t *)dev(h_dcap),
-                                (uint32_t *)dev(h_dlen), (int32_t *)dev(h_rc), (uint32_t)max_len, st);
-    if (!r) {
-        HIP_TRY(hipMemcpyAsync(h_dlen, dev(h_dlen), al256(m * 4ull) * 2, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-    }
-    std::lock_guard<std::mutex> a(s->alloc_mu);
-    for (uint32_t k = 0; k < m; k++) {
-        const uint32_t i = pick[k];
-        const int code = r ? r : h_rc[k];
-        if (code != PMC_OK) {
-            store_release(s, ext[i]);
-            rc[i] = code;
-            continue;
+    auto ok = [](hipError_t e) {
+        if (e != hipSuccess) set_err("pmc_store_put_batch", e);
+        return e == hipSuccess;
+    };
+    // 1. values in, members into the staging slots, lengths back
+    if (!ok(hipMemcpyAsync(dp, hp, meta + bytes, hipMemcpyHostToDevice, st))) return fail_all(PMC_E_NO_DEVICE);
+    r = pmc_gzip_compress_batch(ctx, dev(h_src), (uint64_t *)dev(h_soff), (uint32_t *)dev(h_slen), m, d_slots,
+                                (uint64_t *)dev(h_doff), (uint32_t *)dev(h_dcap), (uint32_t *)dev(h_dlen),
+                                (int32_t *)dev(h_rc), (uint32_t)max_len, st);
+    if (r) return fail_all(r);
+    if (!ok(hipMemcpyAsync(h_dlen, dev(h_dlen), al256(m * 4ull) * 2, hipMemcpyDeviceToHost, st)) ||
+        !ok(hipStreamSynchronize(st)))
+        return fail_all(PMC_E_NO_DEVICE);
+    // 2. extents by compressed length
+    {
+        std::lock_guard<std::mutex> a(s->alloc_mu);
+        for (uint32_t k = 0; k < m; k++) {
+            const uint32_t i = pick[k];
+            if (h_rc[k] != PMC_OK) {
+                rc[i] = h_rc[k];
+                continue;
+            }
+            const uint32_t size = extent_size(h_dlen[k]);
+            uint64_t off = 0;
+            if (!store_alloc(s, size, &off)) {
+                rc[i] = h_rc[k] = PMC_Z_MEM_ERROR;  // the compact pass skips it
+                continue;
+            }
+            ext[i] = pmc_extent{off, size, h_dlen[k], src_len[i], 1};
+            h_poff[k] = off;
         }
-        ext[i].len = h_dlen[k];
     }
-    return r;
+    // 3. members from the slots into their extents (one H2D of the extent offsets and verdicts)
+    bool moved = ok(hipMemcpyAsync(dev(h_poff), h_poff, m * 8ull, hipMemcpyHostToDevice, st)) &&
+                 ok(hipMemcpyAsync(dev(h_rc), h_rc, m * 4ull, hipMemcpyHostToDevice, st));
+    if (moved) {
+        hipLaunchKernelGGL(compact_kernel, dim3(std::min<uint32_t>((m + 3) / 4, 8192)), dim3(256), 0, st,
+                           (const uint8_t *)d_slots, (const uint64_t *)dev(h_doff), (const uint32_t *)dev(h_dlen),
+                           (const int32_t *)dev(h_rc), (const uint64_t *)dev(h_poff), m, (uint8_t *)s->heap.p);
+        moved = ok(hipGetLastError()) && ok(hipStreamSynchronize(st));
+    }
+    if (!moved) {  // the extents hold nothing: release them and fail their values
+        std::lock_guard<std::mutex> a(s->alloc_mu);
+        for (uint32_t k = 0; k < m; k++) {
+            const uint32_t i = pick[k];
+            if (ext[i].flags & 1) store_release(s, ext[i]);
+            rc[i] = PMC_E_NO_DEVICE;
+        }
+        return PMC_E_NO_DEVICE;
+    }
+    return PMC_OK;
 }
 
 PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n, int frame, const uint8_t **resp,
@@ -442,6 +471,7 @@ PMC_API int pmc_slab_set(pmc_slab *s, const uint8_t *src, const uint64_t *src_of
     pmc_ctx *ctx = s->ctx;
     hipStream_t st = (hipStream_t)stream;
     // the set scratch follows the compress direction's ordering (dir_enter / dir_leave)
+    std::lock_guard<std::recursive_mutex> dir_lock(ctx->dir_mu[0]);
     int r = dir_enter(ctx, 0, st);
     if (r) return r;
     const uint64_t a8 = ((uint64_t)n * 8 + 255) & ~(uint64_t)255, a4 = ((uint64_t)n * 4 + 255) & ~(uint64_t)255;
@@ -465,6 +495,7 @@ PMC_API int pmc_slab_get(pmc_slab *s, const uint32_t *slot, uint32_t n, uint8_t 
     if (n == 0) return PMC_OK;
     pmc_ctx *ctx = s->ctx;
     hipStream_t st = (hipStream_t)stream;
+    std::lock_guard<std::recursive_mutex> dir_lock(ctx->dir_mu[1]);
     int r = dir_enter(ctx, 1, st);
     if (r) return r;
     const uint64_t a8 = ((uint64_t)n * 8 + 255) & ~(uint64_t)255;

@@ -101,13 +101,40 @@ std::vector<char *> DecompressForGet(const std::vector<Entry> &entries, std::vec
                                                  (uint32_t)pick.size(), dst.data(), dst_off.data(), dst_cap.data(),
                                                  dst_len.data(), rc.data())
                 : PMC_E_NO_DEVICE;
-    for (size_t k = 0; k < pick.size(); k++) {
-        if (r || rc[k] != OPERATION_SUCCESS) continue;
-        char *v = new char[dst_len[k] + 1];
-        memcpy(v, dst.data() + dst_off[k], dst_len[k]);
-        v[dst_len[k]] = '\0';
+    auto place = [&](size_t k, const uint8_t *bytes, uint32_t len) {
+        char *v = new char[len + 1];
+        memcpy(v, bytes, len);
+        v[len] = '\0';
         out[pick[k]] = v;
         if (owned) (*owned)[pick[k]] = true;
+    };
+    std::vector<uint32_t> again;
+    for (size_t k = 0; k < pick.size(); k++) {
+        if (r) break;
+        if (rc[k] == OPERATION_SUCCESS) place(k, dst.data() + dst_off[k], dst_len[k]);
+        else if (rc[k] == PMC_E_CAPACITY && dst_len[k] > dst_cap[k]) again.push_back((uint32_t)k);
+    }
+    // members followed by bytes that misstate their size (the reference ignores bytes after the
+    // first member, gzip_compressor.cpp:96): PMC_E_CAPACITY carries the decoded size, so one more
+    // call with exactly that room gives their bytes or their verdict
+    if (!again.empty()) {
+        std::vector<uint64_t> s2_off, d2_off;
+        std::vector<uint32_t> s2_len, d2_cap, d2_len(again.size());
+        std::vector<int32_t> rc2(again.size(), 0);
+        uint64_t d2 = 0;
+        for (uint32_t k : again) {
+            s2_off.push_back(src_off[k]);
+            s2_len.push_back(src_len[k]);
+            d2_off.push_back(d2);
+            d2_cap.push_back(dst_len[k]);
+            d2 += dst_len[k];
+        }
+        std::vector<uint8_t> dst2(d2 + 1);
+        const int r2 = pmc_gzip_decompress_batch_host(ctx, src.data(), s2_off.data(), s2_len.data(),
+                                                      (uint32_t)again.size(), dst2.data(), d2_off.data(),
+                                                      d2_cap.data(), d2_len.data(), rc2.data());
+        for (size_t j = 0; j < again.size() && !r2; j++)
+            if (rc2[j] == OPERATION_SUCCESS) place(again[j], dst2.data() + d2_off[j], d2_len[j]);
     }
     return out;
 }

@@ -31,17 +31,24 @@ CompressResult GzipCompressor::Compress(const char *input) {
 
 DecompressResult GzipCompressor::Decompress(const char *input, size_t input_size) {
     if (!input || input_size == 0) return {nullptr, INVALID_INPUT};
-    // ISIZE sizes the output; a lying ISIZE makes the stream fail its length check (-3).
-    // DEFLATE expands at most 1032:1, so a larger ISIZE cannot belong to a valid member.
+    // First guess: the ISIZE trailer (the input's last 4 bytes), clamped to DEFLATE's 1032:1
+    // maximum expansion.  Bytes after the member (the reference ignores them, gzip_compressor.cpp:96)
+    // make that guess wrong; the codec then reports PMC_E_CAPACITY with the decoded size and the
+    // call is repeated with exactly that room -- the reference's doubling buffer (:71-77) never
+    // turns a size into a verdict either.
     size_t cap = pmc_gzip_isize(input, input_size);
     if (cap > 1032 * input_size + 64) cap = 1032 * input_size + 64;
-    char *out = new char[cap + 1];
-    size_t n = 0;
-    int rc = pmc_gzip_decompress(pmc_default_ctx(), input, input_size, out, cap, &n);
-    if (rc != OPERATION_SUCCESS) {
+    for (int attempt = 0; attempt < 2; attempt++) {
+        char *out = new char[cap + 1];
+        size_t n = 0;
+        int rc = pmc_gzip_decompress(pmc_default_ctx(), input, input_size, out, cap, &n);
+        if (rc == OPERATION_SUCCESS) {
+            out[n] = '\0';
+            return {out, OPERATION_SUCCESS};
+        }
         delete[] out;
-        return {nullptr, rc};
+        if (rc != PMC_E_CAPACITY || n <= cap) return {nullptr, rc};
+        cap = n;
     }
-    out[n] = '\0';
-    return {out, OPERATION_SUCCESS};
+    return {nullptr, PMC_E_CAPACITY};
 }

@@ -160,6 +160,8 @@ class Context:
         if rc != 0:
             raise CodecUnavailable(f"pmc_ctx_create({device}) = {rc}: {last_error()}")
         self.device = device
+        import weakref
+        self._deps = weakref.WeakSet()  # stores / slabs on this context: closed before it
 
     def profile(self, enable: bool):
         """Bracket every kernel the batched calls enqueue with HIP events (diagnostics)."""
@@ -177,6 +179,8 @@ class Context:
 
     def close(self):
         if self.handle:
+            for d in list(getattr(self, "_deps", ())):
+                d.close()
             lib().pmc_ctx_destroy(self.handle)
             self.handle = _p()
 
@@ -222,8 +226,17 @@ class Context:
         if r != 0:
             raise CodecUnavailable(f"batch call failed {r}: {last_error()}")
         raw = dst.raw
-        return [(int(rc[i]), raw[int(dst_off[i]):int(dst_off[i]) + int(dst_len[i])] if rc[i] == 0 else b"")
-                for i in range(n)]
+        res = [(int(rc[i]), raw[int(dst_off[i]):int(dst_off[i]) + int(dst_len[i])] if rc[i] == 0 else b"")
+               for i in range(n)]
+        if not compress and caps is None:
+            # bytes after a member misstated its size (the reference ignores them,
+            # gzip_compressor.cpp:96): PMC_E_CAPACITY carries the decoded size; decode those again
+            again = [i for i in range(n) if rc[i] == E_CAPACITY and int(dst_len[i]) > int(cap[i])]
+            if again:
+                redo = self._host_batch([items[i] for i in again], False, [int(dst_len[i]) for i in again])
+                for i, r in zip(again, redo):
+                    res[i] = r
+        return res
 
     # ---------------- device-resident batches (the hot path) ------------------------
     def compress_device(self, src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, max_len, stream=0):
@@ -298,6 +311,7 @@ class Store:
         rc = lib().pmc_store_create(ctx.handle, heap_bytes, ctypes.byref(self.handle))
         if rc != 0:
             raise CodecUnavailable(f"pmc_store_create = {rc}: {last_error()}")
+        ctx._deps.add(self)
 
     def put(self, values):
         """values: list of bytes -> (Extent array, rc list)."""
@@ -373,6 +387,7 @@ class Slab:
         rc = lib().pmc_slab_create(ctx.handle, slots, max_value_len, ctypes.byref(self.handle))
         if rc != 0:
             raise CodecUnavailable(f"pmc_slab_create = {rc}: {last_error()}")
+        ctx._deps.add(self)
         self.stride = lib().pmc_slab_stride(self.handle)
         self.slots = slots
 

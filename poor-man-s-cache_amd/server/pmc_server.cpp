@@ -328,6 +328,7 @@ void Server::apply(Req &q, std::string_view payload) {
         if (codec != Codec::kOff && val.size() + 1 >= kMinCompress) {
             if (codec == Codec::kBatch) {
                 e.kind = kPending;
+                std::string().swap(e.bytes);  // an earlier raw / host-gzip value leaves host memory
                 e.put = (uint32_t)gpus[g].puts.size();
                 gpus[g].puts.push_back(Put{key, val});
             } else {  // single-value call, as the unchanged server through the drop-in
@@ -482,6 +483,7 @@ void Server::run_codec() {
             if (ok) {
                 it->second.kind = kDevice;
                 it->second.ext = g.put_ext[j];
+                std::string().swap(it->second.bytes);
                 st.compressed++;
             } else {
                 it->second.kind = kRaw;

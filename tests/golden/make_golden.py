@@ -126,11 +126,17 @@ def main():
     errs = []
 
     def err(name, data, truncated=False):
+        out = None
         if truncated:
             rc = -5
         else:
-            rc, _ = O.ref_decompress(data)
-        errs.append({"name": name, "hex": data.hex(), "expect_rc": rc, "truncated": truncated})
+            rc, out = O.ref_decompress(data)
+        e = {"name": name, "hex": data.hex(), "expect_rc": rc, "truncated": truncated}
+        if rc == 0:
+            # the reference returns a NUL-terminated buffer and no size (gzip_compressor.cpp:105-110);
+            # every member here decodes to NUL-free text, so its bytes are the C string
+            e["expect_hex"] = out.hex()
+        errs.append(e)
 
     err("not a gzip string (gzip_compressor_test.cpp:90)", b"Not a gzip string")
     err("bad magic", b"\x1f\x8c" + z[2:])
@@ -144,6 +150,22 @@ def main():
     err("invalid block type", z[:10] + bytes([z[10] | 0x06]) + z[11:])
     for k in (1, 4, 8, 9, 12, len(zj) // 2, len(zj) - 5, len(zj) - 1):
         err("truncated to %d" % k, zj[:k], truncated=True)
+    # bytes after the first member (the reference stops at Z_STREAM_END, gzip_compressor.cpp:96):
+    # the input's last 4 bytes no longer hold the member's ISIZE, so any capacity taken from them
+    # is wrong -- smaller, zero, misaligned or larger than the output
+    z50 = O.ref_compress(corpus[5000:5050])[1]
+    zq = O.ref_compress(corpus[20000:20256])[1]
+    err("1 KiB member + 50 B member", zj + z50)
+    err("1 KiB member + 4 NUL bytes", zj + b"\0\0\0\0")
+    for k in (1, 2, 3):
+        err("1 KiB member + %d stray byte(s)" % k, zj + bytes(range(1, k + 1)))
+    err("1 KiB member + bytes reading as a larger ISIZE", zj + (5000).to_bytes(4, "little"))
+    err("1 KiB member + bytes reading as ISIZE 2^32-1", zj + b"\xff\xff\xff\xff")
+    err("256 B member + 4 NUL bytes", zq + b"\0\0\0\0")
+    err("short member + 4 NUL bytes", z + b"\0\0\0\0")
+    err("1 KiB member + truncated member", zj + zj[:40])
+    err("CRC-flipped 1 KiB member + 4 NUL bytes", zj[:-8] + bytes([zj[-8] ^ 1]) + zj[-7:] + b"\0\0\0\0")
+    err("ISIZE-flipped 1 KiB member + 50 B member", zj[:-4] + bytes([zj[-4] ^ 1]) + zj[-3:] + z50)
 
     index = {
         "generator": "tests/golden/make_golden.py",

@@ -1,7 +1,7 @@
 // batch_codec_test.cpp -- pmc_batch::CompressForSet / DecompressForGet (the codec half of a
 // batched server path) against the reference's per-value kvs decisions
 // (/root/reference/src/kvs/kvs.cpp:148,182-196,224,233-234) and the reference's bytes.
-// usage: batch_codec_test <tests/golden/data dir> <golden gz dir>
+// usage: batch_codec_test <tests/golden/data dir> <golden gz dir> [<decompress vector dir>]
 #include <cstdio>
 #include <cstring>
 #include <dirent.h>
@@ -98,6 +98,35 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < got.size(); i++)
         if (owned[i]) delete[] got[i];
     for (auto &r : res) delete[] r.data;
+    // GET batch of tests/golden's decompress vectors (argv[3], as dropin_test): the reference's bytes
+    // (nullptr for its error verdicts), members followed by ignored bytes included
+    if (argc >= 4) {
+        std::string vdir = argv[3];
+        FILE *ix = fopen((vdir + "/dec_index.txt").c_str(), "r");
+        int k = 0, want_rc = 0;
+        std::vector<std::string> ins, wants;
+        std::vector<int> rcs;
+        while (ix && fscanf(ix, "%d %d", &k, &want_rc) == 2) {
+            if (want_rc == -5) continue;  // truncated: the drop-in's documented -5, nullptr here too
+            ins.push_back(slurp(vdir + "/dec_" + std::to_string(k) + ".gz"));
+            wants.push_back(want_rc == 0 ? slurp(vdir + "/dec_" + std::to_string(k) + ".out") : "");
+            rcs.push_back(want_rc);
+        }
+        if (ix) fclose(ix);
+        EXPECT(!ins.empty());
+        std::vector<pmc_batch::Entry> dents;
+        for (auto &x : ins) dents.push_back({x.data(), x.size(), true});
+        std::vector<bool> down;
+        auto dgot = pmc_batch::DecompressForGet(dents, &down);
+        for (size_t i = 0; i < ins.size(); i++) {
+            if (rcs[i] == 0) {
+                EXPECT(dgot[i] && strlen(dgot[i]) == wants[i].size() && memcmp(dgot[i], wants[i].data(), wants[i].size()) == 0);
+            } else {
+                EXPECT(dgot[i] == nullptr);
+            }
+            if (down[i]) delete[] dgot[i];
+        }
+    }
     // compression disabled: everything stored raw
     auto raw = pmc_batch::CompressForSet({vals[0], vals[1]}, false);
     EXPECT(!raw[0].compressed && raw[0].size == strlen(vals[0]) + 1);

@@ -2,7 +2,7 @@
 // KeyValueStoreTest.LargeJSONFiles (kvs_test.cpp:36-65), re-expressed without gtest, run
 // against the drop-in GzipCompressor (poor-man-s-cache_amd/dropin) on the GPU.
 // Additionally every compressed buffer is compared with the golden bytes passed on argv.
-// usage: dropin_test <tests/golden/data dir> <golden gz dir>
+// usage: dropin_test <tests/golden/data dir> <golden gz dir> [<decompress vector dir>]
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -112,6 +112,30 @@ int main(int argc, char **argv) {
         }
         if (dp) closedir(dp);
         EXPECT(files == 6);
+    }
+    // Decompress verdicts and bytes of tests/golden's decompress vectors (argv[3]: dec_index.txt with
+    // "k rc" lines, dec_k.gz the input, dec_k.out the reference's output), including members followed
+    // by bytes the reference ignores (gzip_compressor.cpp:96)
+    if (argc >= 4) {
+        std::string vdir = argv[3];
+        FILE *ix = fopen((vdir + "/dec_index.txt").c_str(), "r");
+        int k = 0, want_rc = 0, nvec = 0;
+        while (ix && fscanf(ix, "%d %d", &k, &want_rc) == 2) {
+            std::string in = slurp(vdir + "/dec_" + std::to_string(k) + ".gz");
+            auto d = GzipCompressor::Decompress(in.data(), in.size());
+            if (d.operationResult != want_rc) fprintf(stderr, "vector %d: rc %d, want %d\n", k, d.operationResult, want_rc);
+            EXPECT(d.operationResult == want_rc);
+            if (want_rc == OPERATION_SUCCESS) {
+                std::string want = slurp(vdir + "/dec_" + std::to_string(k) + ".out");
+                EXPECT(d.data && strlen(d.data) == want.size() && memcmp(d.data, want.data(), want.size()) == 0);
+            } else {
+                EXPECT(d.data == nullptr);
+            }
+            delete[] d.data;
+            nvec++;
+        }
+        if (ix) fclose(ix);
+        EXPECT(nvec > 0);
     }
     printf("dropin_test: %d failure(s)\n", failures);
     return failures ? 1 : 0;

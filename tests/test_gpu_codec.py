@@ -68,14 +68,65 @@ def test_decompress_all_golden_vectors(ctx, D, golden):
     assert not bad, f"{len(bad)} vectors differ; first {bad[:8]}"
 
 
+def write_decompress_vectors(golden, d):
+    """tests/golden's decompress vectors as files for the C++ drivers (dec_index.txt: "k rc")."""
+    with open(os.path.join(d, "dec_index.txt"), "w") as ix:
+        for k, e in enumerate(golden.index["decompress_errors"]):
+            with open(os.path.join(d, "dec_%d.gz" % k), "wb") as f:
+                f.write(bytes.fromhex(e["hex"]))
+            if e["expect_rc"] == 0:
+                with open(os.path.join(d, "dec_%d.out" % k), "wb") as f:
+                    f.write(bytes.fromhex(e["expect_hex"]))
+            ix.write("%d %d\n" % (k, e["expect_rc"]))
+
+
 def test_decompress_error_verdicts(ctx, D, golden):
+    """The reference's verdict AND bytes for every decompress vector, including members followed by
+    bytes it ignores (gzip_compressor.cpp:96).  Device batch with ISIZE capacities: a member whose
+    last 4 input bytes understate its output reports PMC_E_CAPACITY and its decoded size, and the
+    second call with exactly that room gives the reference's answer."""
+    import pmc_codec
     errs = golden.index["decompress_errors"]
-    b = D.pack([bytes.fromhex(e["hex"]) for e in errs])
+    vecs = [bytes.fromhex(e["hex"]) for e in errs]
+    b = D.pack(vecs)
     out, rc = D.decompress(ctx, b)
     sync()
     rc = rc.cpu().numpy()
+    dlen = out.len.cpu().numpy()
+    got = out.host_items()
+    redo = []
     for k, e in enumerate(errs):
+        if rc[k] == pmc_codec.E_CAPACITY:
+            assert dlen[k] > pmc_codec.decompress_capacity(vecs[k]), e["name"]
+            if e["expect_rc"] == 0:
+                assert dlen[k] == len(e["expect_hex"]) // 2, e["name"]
+            redo.append(k)
+            continue
         assert rc[k] == e["expect_rc"], (e["name"], rc[k])
+        if e["expect_rc"] == 0:
+            assert got[k] == bytes.fromhex(e["expect_hex"]), e["name"]
+    assert redo, "the trailing-bytes vectors should need a second call"
+    b2 = D.pack([vecs[k] for k in redo])
+    out2, rc2 = D.decompress(ctx, b2, [int(dlen[k]) for k in redo])
+    sync()
+    rc2 = rc2.cpu().numpy()
+    got2 = out2.host_items()
+    for j, k in enumerate(redo):
+        e = errs[k]
+        assert rc2[j] == e["expect_rc"], (e["name"], rc2[j])
+        if e["expect_rc"] == 0:
+            assert got2[j] == bytes.fromhex(e["expect_hex"]), e["name"]
+    # host batch API (grows and retries itself) and the Python GzipCompressor mirror
+    for k, (r, data) in enumerate(ctx.decompress_many(vecs)):
+        e = errs[k]
+        assert r == e["expect_rc"], (e["name"], r)
+        assert data == (bytes.fromhex(e["expect_hex"]) if r == 0 else b""), e["name"]
+    for k, e in enumerate(errs):
+        if e["truncated"]:
+            continue
+        d = pmc_codec.GzipCompressor.Decompress(vecs[k], len(vecs[k]))
+        assert d.operationResult == e["expect_rc"], e["name"]
+        assert d.data == (bytes.fromhex(e["expect_hex"]) if e["expect_rc"] == 0 else None), e["name"]
 
 
 def test_corruption_fuzz_matches_oracle(ctx, D):
@@ -98,12 +149,27 @@ def test_corruption_fuzz_matches_oracle(ctx, D):
     out, rc = D.decompress(ctx, b, caps)
     sync()
     rc = rc.cpu().numpy()
+    dlen = out.len.cpu().numpy()
     got = out.host_items()
+    redo = []
     for k, v in enumerate(vecs):
-        erc, eout = O.decompress(v, cap=max(caps[k], 1))
+        erc, eout = O.decompress(v, cap=caps[k], grow=False)
         assert rc[k] == erc, (k, rc[k], erc)
         if erc == 0:
             assert got[k] == eout
+        if erc == pmc_codec.E_CAPACITY:
+            redo.append(k)
+    # a corrupted ISIZE understates the output: the decoded size comes back, the second call decides
+    if redo:
+        out2, rc2 = D.decompress(ctx, D.pack([vecs[k] for k in redo]), [int(dlen[k]) for k in redo])
+        sync()
+        rc2 = rc2.cpu().numpy()
+        got2 = out2.host_items()
+        for j, k in enumerate(redo):
+            erc, eout = O.decompress(vecs[k])
+            assert rc2[j] == erc, (k, rc2[j], erc)
+            if erc == 0:
+                assert got2[j] == eout
 
 
 def test_digest_sets_generated_on_device(ctx, D, golden):
@@ -260,12 +326,13 @@ def test_cpp_dropin_links_and_passes(ctx, golden):
         assert r == data
         with open(os.path.join(d, name + ".gz"), "wb") as f:
             f.write(g)
+    write_decompress_vectors(golden, d)
     exe = os.path.join(d, "dropin_test")
     pkg = os.path.dirname(pmc_codec.LIB_PATH)
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "poor-man-s-cache_amd", "dropin"),
                            "-o", exe, os.path.join(ROOT, "tests", "host", "dropin_test.cpp"),
                            "-L", pkg, "-lgzip_dropin", "-lpmc_codec", "-Wl,-rpath," + pkg])
-    r = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "data"), d], capture_output=True, text=True,
+    r = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "data"), d, d], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
 
@@ -279,12 +346,13 @@ def test_batch_codec_set_get(ctx, golden):
         r, g = golden.pair(k)
         with open(os.path.join(d, name + ".gz"), "wb") as f:
             f.write(g)
+    write_decompress_vectors(golden, d)
     exe = os.path.join(d, "batch_codec_test")
     pkg = os.path.dirname(pmc_codec.LIB_PATH)
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "poor-man-s-cache_amd", "dropin"),
                            "-o", exe, os.path.join(ROOT, "tests", "host", "batch_codec_test.cpp"),
                            "-L", pkg, "-lgzip_dropin", "-lpmc_codec", "-Wl,-rpath," + pkg])
-    r = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "data"), d], capture_output=True, text=True,
+    r = subprocess.run([exe, os.path.join(ROOT, "tests", "golden", "data"), d, d], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
 

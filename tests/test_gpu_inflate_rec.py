@@ -80,7 +80,8 @@ def test_record_inflate_mixed_sizes_unaligned_slots(golden):
 
 
 def test_record_inflate_capacity_and_corrupt_verdicts(golden):
-    """Output capacity one short of ISIZE, a lying ISIZE, a corrupt distance: zlib's verdicts."""
+    """Output capacity one short of ISIZE (PMC_E_CAPACITY + the decoded size), a lying ISIZE, a
+    corrupt distance: zlib's verdicts."""
     import torch
     import pmc_codec
     from pmc_codec import device as D
@@ -120,9 +121,17 @@ def test_record_inflate_capacity_and_corrupt_verdicts(golden):
     finally:
         ctx.close()
     rc = rc.cpu().numpy()
+    dl = dlen.cpu().numpy()
     got = D.Batch(dst, doff, dlen, n, 0).host_items()
+    short = 0
     for k, v in enumerate(vecs):
-        erc, eout = O.decompress(v, cap=max(caps[k], 1))
+        erc, eout = O.decompress(v, cap=caps[k], grow=False)
         assert rc[k] == erc, (k, caps[k], int(rc[k]), erc)
         if erc == 0:
             assert got[k] == eout, k
+        if erc == pmc_codec.E_CAPACITY:
+            # no verdict yet: the decoded size comes back, and exactly that much room suffices
+            short += 1
+            assert dl[k] > caps[k], k
+            assert O.decompress(v, cap=int(dl[k]), grow=False)[0] != O.CAPACITY, k
+    assert short >= 7  # every "one short" member

@@ -67,11 +67,38 @@ def test_store_free_reuse_and_full_heap(ctx, golden):
     assert [g for _, g in st.get(odd, k)] == [vals[i] for i in range(1, len(vals), 2)]
     # a freed extent is not readable; a heap that cannot hold a value fails that value only
     assert st.get(half, 1)[0][0] == pmc_codec.E_ARG
+    import numpy as np
     small = pmc_codec.Store(ctx, 4096)
-    e3, rc3 = small.put([b"x" * 100, bytes(range(1, 256)) * 40, b"y" * 200])
+    noise = bytes(np.random.default_rng(3).integers(0, 256, 6000, dtype=np.uint8))  # stored blocks: > 4 KiB
+    e3, rc3 = small.put([b"x" * 100, noise, b"y" * 200])
     assert rc3[0] == 0 and rc3[1] == pmc_codec.Z_MEM_ERROR and rc3[2] == 0
     assert [g for _, g in small.get(e3, 3)][0::2] == [b"x" * 100, b"y" * 200]
     assert small.get(e3, 3)[1][0] == pmc_codec.E_ARG
+
+
+def test_store_footprint_is_compressed_size(ctx, golden):
+    """Extents are sized by the member, not by the uncompressed bound (the reference's Entry holds the
+    compressed bytes, kvs.hpp:38-44): used == sum of 16-byte-rounded member sizes.  A put that cannot
+    place a value (heap full) leaves `used` unchanged."""
+    import pmc_codec
+    pairs = [(r, g) for r, g in golden.pairs() if 0 < len(r) <= 4096]
+    st = pmc_codec.Store(ctx, 16 << 20)
+    ext, rc = st.put([r for r, _ in pairs])
+    assert rc == [0] * len(pairs)
+    want = sum((len(g) + 15) & ~15 for _, g in pairs)
+    assert st.stats()["used"] == want
+    bound = sum((pmc_codec.gzip_bound(len(r)) + 15) & ~15 for r, _ in pairs)
+    assert want < 0.75 * bound
+    assert [ext[i].len for i in range(len(pairs))] == [len(g) for _, g in pairs]
+    full = pmc_codec.Store(ctx, 4096)
+    e1, r1 = full.put([b"z" * 3000])
+    assert r1 == [0]
+    u = full.stats()["used"]
+    import numpy as np
+    noise = bytes(np.random.default_rng(4).integers(0, 256, 8000, dtype=np.uint8))
+    e2, r2 = full.put([noise, noise])
+    assert r2 == [pmc_codec.Z_MEM_ERROR] * 2 and full.stats()["used"] == u
+    assert e2[0].flags == 0 and e2[1].flags == 0
 
 
 def _d2h(ptr, nbytes):

@@ -28,9 +28,20 @@ def test_inflate_roundtrips_goldens(golden):
 
 
 def test_decompress_error_verdicts(golden):
+    """The reference's verdict and bytes for every decompress vector: with a roomy buffer, and with
+    the ISIZE-sized first guess that members followed by extra bytes overflow (capacity is then
+    reported with the decoded size, never as a verdict)."""
+    grew = 0
     for e in golden.index["decompress_errors"]:
-        rc, _ = O.decompress(bytes.fromhex(e["hex"]), cap=1 << 16)
-        assert rc == e["expect_rc"], e["name"]
+        v = bytes.fromhex(e["hex"])
+        want = bytes.fromhex(e["expect_hex"]) if e["expect_rc"] == 0 else b""
+        for cap in (1 << 16, None):
+            rc, out = O.decompress(v, cap=cap)
+            assert rc == e["expect_rc"], (e["name"], cap, rc)
+            assert out == want, (e["name"], cap)
+        rc, _ = O.decompress(v, grow=False)
+        grew += rc == O.CAPACITY
+    assert grew >= 4
 
 
 def test_generator_pins_golden_sets(golden):
