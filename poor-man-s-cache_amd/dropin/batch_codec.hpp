@@ -11,11 +11,14 @@
 // pmc_gzip_*_batch_host call each.
 #pragma once
 #include <cstddef>
+#include <string_view>
 #include <vector>
 
-#include "gzip_compressor.hpp"
-
+// (gzip_compressor.hpp is not included here: a TU that also sees the reference's own copy of that
+// header through src/kvs -- the f1 server hook -- would get its structs twice)
 struct pmc_ctx;
+struct CompressResult;
+struct DecompressResult;
 
 namespace pmc_batch {
 
@@ -49,5 +52,42 @@ struct Entry {
 /// whether result i is a new[] buffer the caller must delete[].
 std::vector<char *> DecompressForGet(const std::vector<Entry> &entries, std::vector<bool> *owned = nullptr,
                                      pmc_ctx *ctx = nullptr);
+
+// ---- f1 inside the UNCHANGED caller: priming GzipCompressor for one request batch ----------------
+// kvs.cpp keeps calling GzipCompressor::Compress / ::Decompress one value at a time (:183, :233).  A
+// server loop that knows its batch (the epoll iteration, server.cpp:361-390) primes those calls first:
+// every value of the batch is compressed (and every member decompressed) by ONE device batch call,
+// and the per-value calls that follow are answered from the primed results.  State is per thread
+// (the reference serves requests on one thread, server.cpp:631-643) and lives until EndBatch().
+
+/// Compress the batch's SET values (the C strings Compress will be called with: strlen'd bytes,
+/// values shorter than kMinCompressSize - 1 are skipped).  A later Compress(v) with the same bytes
+/// gets the primed member (matched by content: kvs copies the value before compressing it).
+void PrimeCompress(const std::vector<std::string_view> &values, pmc_ctx *ctx = nullptr);
+
+/// Between BeginCollect() and PrimeCollected(), Decompress(ptr, size) only records (ptr, size) and
+/// returns {nullptr, INVALID_INPUT}: a dry run of the batch's GETs (kvs::get is a pure lookup)
+/// learns which stored members they will decompress.  PrimeCollected() decompresses them in one
+/// device call; a later Decompress(ptr, size) of the same stored bytes gets the primed value
+/// (matched by pointer, size and content, so a buffer freed and reused meanwhile never matches).
+void BeginCollect();
+void PrimeCollected(pmc_ctx *ctx = nullptr);
+
+/// Drop the primed results the batch did not use (their buffers are freed).
+void EndBatch();
+
+/// Counters of the calling thread: primed compress / decompress results handed out, and calls that
+/// found no primed result (ran the single-value path).
+struct PrimeStats {
+    size_t compress_hits, compress_misses, decompress_hits, decompress_misses, batches;
+};
+PrimeStats GetPrimeStats();
+
+namespace detail {
+// used by GzipCompressor (gzip_compressor.cpp)
+bool TakeCompressed(const char *input, size_t len, CompressResult *out);
+bool Collecting(const char *input, size_t size);
+bool TakeDecompressed(const char *input, size_t size, DecompressResult *out);
+} // namespace detail
 
 } // namespace pmc_batch

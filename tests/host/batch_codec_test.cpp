@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "batch_codec.hpp"
+#include "gzip_compressor.hpp"
 
 static int failures = 0;
 #define EXPECT(c)                                                            \

@@ -1,0 +1,120 @@
+"""The reference's OWN cache server over the codec boundary (BASELINE configs[4]).
+
+oracle/Makefile `server` compiles /root/reference/src/server, kvs, hash, primegen and utils unmodified
+where they lie, with a build-owned main that leaves out only the Prometheus exposer
+(poor-man-s-cache_amd/server/ref_main.cpp), into three binaries that differ only in the codec under kvs:
+  ref_server_zlib    the reference's own gzip_compressor.cpp + zlib (the reference as deployed)
+  ref_server_dropin  the drop-in GzipCompressor: one GPU call per value (kvs.cpp:183, :233)
+  ref_server_batch   the drop-in + ref_server_batch.patch + ref_batch_hook.cpp: each epoll iteration's
+                     codec work as one device batch per direction (f1 inside server.cpp:361-390)
+CPU: the reference's own load test, /root/reference/tests/tcp_server_test.py -p -b 100 (run by path,
+in the build container only -- the reference is not on the GPU box), passes against all three (the
+drop-in answers PMC_E_NO_DEVICE without a GPU, so kvs stores those values raw, kvs.cpp:188-191), and
+the protocol checks of test_server.py give the same answers from all three.  GPU: the drop-in and the
+batch binary under pmc_loadgen's pipelined 4 KiB JSON load, every GET checked, and the batch binary's
+priming counters show the device batches answered the codec calls.
+"""
+import json
+import os
+import signal
+import socket
+import subprocess
+import time
+
+import pytest
+
+from test_server import DATA, _exchange, _free_port, _load, _semantics
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_BIN = os.path.join(ROOT, "oracle", "_ref")
+HARNESS = "/root/reference/tests/tcp_server_test.py"
+
+
+class RefServer:
+    def __init__(self, kind, tmp_path=None, shards=128):
+        exe = os.path.join(REF_BIN, "ref_server_" + kind)
+        if not os.path.exists(exe):
+            pytest.skip(f"{exe} not built (make -C oracle server, needs /root/reference)")
+        self.port = _free_port()
+        env = dict(os.environ, SERVER_PORT=str(self.port), NUM_SHARDS=str(shards))  # .env:4 deploys 128
+        self.stats = None
+        if tmp_path is not None:
+            self.stats = str(tmp_path / f"prime_{kind}.json")
+            env["PMC_PRIME_STATS"] = self.stats
+        self.p = subprocess.Popen([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        t0 = time.time()
+        while True:
+            try:
+                socket.create_connection(("127.0.0.1", self.port), timeout=1).close()
+                break
+            except OSError:
+                assert self.p.poll() is None, self.p.stderr.read()
+                assert time.time() - t0 < 60, "server did not come up"
+                time.sleep(0.05)
+
+    def stop(self):
+        self.p.send_signal(signal.SIGTERM)  # this exact child: main's handler calls CacheServer::Stop
+        try:
+            out, err = self.p.communicate(timeout=30)
+        except subprocess.TimeoutExpired:
+            self.p.kill()
+            out, err = self.p.communicate()
+            raise AssertionError("server did not stop on SIGTERM: " + err[-2000:])
+        assert self.p.returncode == 0, err[-2000:]
+        if self.stats and os.path.exists(self.stats):
+            with open(self.stats) as f:
+                return json.load(f)
+        return None
+
+
+@pytest.mark.parametrize("kind", ["zlib", "dropin", "batch"])
+def test_reference_load_test_passes(kind):
+    """tcp_server_test.py -p -b 100 verbatim (BASELINE configs[4]); it exits 1 on any failed request."""
+    if not os.path.exists(HARNESS):
+        pytest.skip("the reference's harness is only in the build container")
+    s = RefServer(kind)
+    try:
+        env = dict(os.environ, CACHE_HOST="127.0.0.1", CACHE_PORT=str(s.port), TEST_DELAY_SEC="0.05",
+                   TEST_POOL_SIZE="4", TEST_DATA_FOLDER=os.path.join(os.path.dirname(HARNESS), "data"))
+        r = subprocess.run(["python3", HARNESS, "-p", "-b", "100"], env=env, cwd=os.path.dirname(HARNESS),
+                           capture_output=True, text=True, timeout=300)
+    finally:
+        s.stop()
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rps = [ln for ln in r.stdout.splitlines() if "RPS:" in ln]
+    assert len(rps) == 4 and all("Failures: 0" in ln for ln in rps), r.stdout
+    print(kind, *rps, sep="\n  ")
+
+
+@pytest.mark.parametrize("kind", ["dropin", "batch"])
+def test_protocol_answers_equal_reference_server(golden, kind):
+    """The same command sequences give the same answers from the reference server over zlib and over the
+    drop-in (test_server._semantics encodes them; here checked against the real server).  Without a GPU
+    the drop-in's values are stored raw, so commands go one per write here: pipelined, a raw GET followed
+    by a SET of the same key reads freed memory in the reference server itself (see _semantics)."""
+    for k in ("zlib", kind):
+        s = RefServer(k)
+        try:
+            _semantics(s.port, golden, one_by_one=True)
+        finally:
+            s.stop()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["dropin", "batch"])
+def test_reference_server_on_gpu_codec(golden, tmp_path, kind):
+    s = RefServer(kind, tmp_path)
+    try:
+        _semantics(s.port, golden)
+        res = _load(s.port, 4096, 40_000 if kind == "batch" else 4_000, keys=8192 if kind == "batch" else 1024)
+        # the JSON files through GET after the load: stored members decode to the reference's bytes
+        files = [d for _, d in golden.data_files]
+        assert _exchange(s.port, [b"SET f%d " % i + d for i, d in enumerate(files)]) == [b"OK"] * len(files)
+        assert _exchange(s.port, [b"GET f%d" % i for i in range(len(files))]) == files
+    finally:
+        st = s.stop()
+    print(kind, res, st)
+    if kind == "batch":
+        assert st and st["batches"] > 0 and st["compress_hits"] > 8192 and st["decompress_hits"] > 1000, st
+        # misses are GETs of keys SET earlier in the same iteration (their entry is newer than the dry run)
+        assert st["compress_misses"] == 0 and st["decompress_misses"] < st["decompress_hits"] // 4, st
