@@ -88,25 +88,25 @@ def load_corpus():
     return b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)) if f.endswith(".json"))
 
 
-def fullsize_bitexact(L, ctx, comp, coff, clen, n, vlen, kind, world, sh):
-    """Byte parity of ALL n members of the run against the reference (tests/golden/full_digests.json,
-    made by tests/golden/make_full_digests.py from the reference's own Compress): the device takes the
-    CRC-32 of every member (pmc_crc32_batch), the host hashes the (length, CRC) records with SHA-256.
-    Returns {"bitexact": bool, ...}, or None when no digest covers this workload (e.g. N > 1 ranks,
-    whose routed key subsets differ)."""
+def fullsize_parity(L, ctx, comp, coff, clen, n, vlen, kind, world, rank, sh):
+    """Parity of ALL n members of this rank's run with the reference (tests/golden/full_digests.json at
+    N = 1, tests/golden/rank_digests.json for rank r of N = 2/4/8; both made by
+    tests/golden/make_full_digests.py from the reference's own Compress): the device takes the CRC-32 of
+    every member (pmc_crc32_batch), the host hashes the (u32 length, u32 CRC-32) records with SHA-256.
+    That is a length + CRC-32 digest of the bytes, not a byte comparison.  Returns {"match": bool, ...},
+    or None when no digest covers this workload."""
     import hashlib
-    import numpy as np
     import torch
-    if world != 1:
-        return None
+    fname = "full_digests.json" if world == 1 else "rank_digests.json"
     try:
-        with open(os.path.join(ROOT, "tests", "golden", "full_digests.json")) as f:
+        with open(os.path.join(ROOT, "tests", "golden", fname)) as f:
             doc = json.load(f)
     except (OSError, ValueError):
         return None
     want = None
     for st in doc["sets"]:
-        if st["vlen"] == vlen and st["kind"] == kind and str(n) in st["prefixes"]:
+        if (st["vlen"] == vlen and st["kind"] == kind and str(n) in st["prefixes"]
+                and (world == 1 or (st.get("world") == world and st.get("rank") == rank))):
             want = st["prefixes"][str(n)]
     if want is None:
         return None
@@ -115,9 +115,10 @@ def fullsize_bitexact(L, ctx, comp, coff, clen, n, vlen, kind, world, sh):
                              sh) == 0
     rec = torch.stack([clen, mcrc], dim=1).cpu().numpy().astype("<u4")
     got = hashlib.sha256(rec.tobytes()).hexdigest()
-    return {"bitexact": got == want["sha256"], "members": n, "sha256": got,
-            "reference": "tests/golden/full_digests.json (reference GzipCompressor::Compress, zlib "
-                         f"{doc.get('zlib_version')}): sha256 over (u32 len, u32 crc32) of every member"}
+    return {"match": got == want["sha256"], "members": n, "sha256": got,
+            "method": "sha256 over the (u32 len, u32 CRC-32) record of every member, vs the reference's",
+            "reference": f"tests/golden/{fname} (reference GzipCompressor::Compress, zlib "
+                         f"{doc.get('zlib_version')})"}
 
 
 def cpu_baseline(corpus, args, index0):
@@ -430,10 +431,16 @@ def main():
     torch.cuda.synchronize()
     bad = int(mism.item()) + int((crc != 0).sum().item()) + int((brc != 0).sum().item())
     comp_bytes = int(clen.to(torch.int64).sum().item())
-    bitexact = fullsize_bitexact(L, ctx, comp, coff, clen, n, vlen, args.kind, world, sh)
+    parity = fullsize_parity(L, ctx, comp, coff, clen, n, vlen, args.kind, world, rank, sh)
 
-    (t_step_s, tc_max, td_max), (total_bytes, total_comp, total_bad) = reduce_over_ranks(
-        [wall / args.steps, tc, td], [float(n * vlen), float(comp_bytes), float(bad)], world, dev)
+    (t_step_s, tc_max, td_max), (total_bytes, total_comp, total_bad, p_match, p_checked) = reduce_over_ranks(
+        [wall / args.steps, tc, td], [float(n * vlen), float(comp_bytes), float(bad),
+                                      float(bool(parity and parity["match"])), float(parity is not None)],
+        world, dev)
+    if world > 1 and parity is not None:  # every rank against its own digest
+        parity = {"match": p_match == world and p_checked == world, "ranks_checked": int(p_checked),
+                  "ranks_matching": int(p_match), "members": n * world, "method": parity["method"],
+                  "reference": parity["reference"]}
 
     # ---- per-kernel launch times of one more step (HIP events around every launch) -----------
     ctx.profile(True)
@@ -498,7 +505,7 @@ def main():
             "decompress_roofline_frac": alg_d / td / 1e9 / HBM_PEAK_GBS,
             "ratio": total_comp / total_bytes, "verified_values": int(total_bytes // vlen),
             "mismatches": int(total_bad),
-            "fullsize_parity": bitexact,
+            "fullsize_parity": parity,
         }
         if h2h:
             out["host_to_host"] = h2h

@@ -68,6 +68,9 @@ uint64_t oracle_splitmix64(uint64_t x);
 uint64_t oracle_murmur3_x64_128_h1(const uint8_t *data, int len, uint32_t seed);
 void oracle_gen_values(const uint8_t *corpus, size_t corpus_len, uint64_t seed, int kind,
                        uint64_t first, uint32_t n, uint32_t vlen, uint8_t *out);
+void oracle_gen_values_idx(const uint8_t *corpus, size_t corpus_len, uint64_t seed, int kind,
+                           const uint64_t *index, uint32_t n, uint32_t vlen, uint8_t *out);
+void oracle_route_keys(uint64_t first, uint64_t n, uint32_t num_shards, uint32_t n_gpus, uint8_t *out);
 
 #ifdef __cplusplus
 }

@@ -48,6 +48,12 @@ def lib():
         L.oracle_gen_values.restype = None
         L.oracle_gen_values.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
                                         ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+        L.oracle_gen_values_idx.restype = None
+        L.oracle_gen_values_idx.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+        L.oracle_route_keys.restype = None
+        L.oracle_route_keys.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_void_p]
         _LIB = L
     return _LIB
 
@@ -108,6 +114,22 @@ def last_stats():
 def gen_values(corpus: bytes, seed: int, kind: int, first: int, n: int, vlen: int) -> np.ndarray:
     out = np.empty((n, vlen), dtype=np.uint8)
     lib().oracle_gen_values(corpus, len(corpus), seed, kind, first, n, vlen,
+                            out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+def gen_values_idx(corpus: bytes, seed: int, kind: int, index: np.ndarray, vlen: int) -> np.ndarray:
+    index = np.ascontiguousarray(index, dtype=np.uint64)
+    out = np.empty((len(index), vlen), dtype=np.uint8)
+    lib().oracle_gen_values_idx(corpus, len(corpus), seed, kind, index.ctypes.data_as(ctypes.c_void_p),
+                                len(index), vlen, out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+def route_keys(first: int, n: int, num_shards: int, n_gpus: int) -> np.ndarray:
+    """hashFunc("key" + i) % num_shards % n_gpus for i in [first, first + n) (server.cpp:113)."""
+    out = np.empty(n, dtype=np.uint8)
+    lib().oracle_route_keys(ctypes.c_uint64(first), ctypes.c_uint64(n), num_shards, n_gpus,
                             out.ctypes.data_as(ctypes.c_void_p))
     return out
 

@@ -69,21 +69,48 @@ uint64_t oracle_murmur3_x64_128_h1(const uint8_t *data, int len, uint32_t seed) 
 
 static const char ALNUM[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789";
 
+static void gen_one(const uint8_t *corpus, size_t corpus_len, uint64_t seed, int kind, uint64_t i, uint32_t vlen,
+                    uint8_t *dst) {
+    if (kind == 0) {
+        uint64_t off = oracle_splitmix64(seed ^ i) % (corpus_len - vlen + 1);
+        for (uint32_t b = 0; b < vlen; b++) dst[b] = corpus[off + b];
+    } else {
+        /* 8-byte group g of value i: st = splitmix64(splitmix64(seed ^ i) + g) */
+        uint64_t hi = oracle_splitmix64(seed ^ i), st = 0;
+        for (uint32_t b = 0; b < vlen; b++) {
+            if ((b & 7) == 0) st = oracle_splitmix64(hi + (b >> 3));
+            dst[b] = (uint8_t)ALNUM[((st >> (8 * (b & 7))) & 0xff) % 62];
+        }
+    }
+}
+
 void oracle_gen_values(const uint8_t *corpus, size_t corpus_len, uint64_t seed, int kind,
                        uint64_t first, uint32_t n, uint32_t vlen, uint8_t *out) {
-    for (uint32_t k = 0; k < n; k++) {
-        uint64_t i = first + k;
-        uint8_t *dst = out + (uint64_t)k * vlen;
-        if (kind == 0) {
-            uint64_t off = oracle_splitmix64(seed ^ i) % (corpus_len - vlen + 1);
-            for (uint32_t b = 0; b < vlen; b++) dst[b] = corpus[off + b];
-        } else {
-            /* 8-byte group g of value i: st = splitmix64(splitmix64(seed ^ i) + g) */
-            uint64_t hi = oracle_splitmix64(seed ^ i), st = 0;
-            for (uint32_t b = 0; b < vlen; b++) {
-                if ((b & 7) == 0) st = oracle_splitmix64(hi + (b >> 3));
-                dst[b] = (uint8_t)ALNUM[((st >> (8 * (b & 7))) & 0xff) % 62];
-            }
-        }
+    for (uint32_t k = 0; k < n; k++) gen_one(corpus, corpus_len, seed, kind, first + k, vlen, out + (uint64_t)k * vlen);
+}
+
+/* the same values at arbitrary global indices (a rank's routed key subset) */
+void oracle_gen_values_idx(const uint8_t *corpus, size_t corpus_len, uint64_t seed, int kind,
+                           const uint64_t *index, uint32_t n, uint32_t vlen, uint8_t *out) {
+    for (uint32_t k = 0; k < n; k++) gen_one(corpus, corpus_len, seed, kind, index[k], vlen, out + (uint64_t)k * vlen);
+}
+
+/* out[i] = hashFunc("key" + (first + i)) % num_shards % n_gpus: the server's shard routing
+ * (/root/reference/src/server/server.cpp:113,121,132; hash.cpp:4-9), what pmc_route_keys computes */
+void oracle_route_keys(uint64_t first, uint64_t n, uint32_t num_shards, uint32_t n_gpus, uint8_t *out) {
+    char key[32];
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t v = first + i;
+        char digits[24];
+        int nd = 0;
+        do {
+            digits[nd++] = (char)('0' + v % 10);
+            v /= 10;
+        } while (v);
+        key[0] = 'k';
+        key[1] = 'e';
+        key[2] = 'y';
+        for (int d = 0; d < nd; d++) key[3 + d] = digits[nd - 1 - d];
+        out[i] = (uint8_t)(oracle_murmur3_x64_128_h1((const uint8_t *)key, 3 + nd, 0) % num_shards % n_gpus);
     }
 }

@@ -14,10 +14,12 @@
 #include <dirent.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -68,20 +70,13 @@ int connect_to(int port) {
     return fd;
 }
 
-bool send_all(int fd, const std::string &s) {
-    size_t o = 0;
-    while (o < s.size()) {
-        const ssize_t w = send(fd, s.data() + o, s.size() - o, MSG_NOSIGNAL);
-        if (w <= 0) return false;
-        o += (size_t)w;
-    }
-    return true;
-}
-
-// reads n responses (0x1F-terminated) into out
-bool recv_n(int fd, std::string &buf, size_t n, std::vector<std::string> &out) {
+// Writes the batch and reads its n responses (0x1F-terminated) into out, reading while it writes: a
+// server that answers the first requests of a batch before it has read the last ones (the reference
+// server sends each epoll iteration's responses before reading again, server.cpp:386-390, and spins on
+// EAGAIN until they are sent) would otherwise deadlock against a client still blocked in send().
+bool exchange(int fd, const std::string &req, std::string &buf, size_t n, std::vector<std::string> &out) {
     out.clear();
-    size_t pos = 0;
+    size_t sent = 0, pos = 0;
     char tmp[1 << 16];
     while (out.size() < n) {
         const size_t e = buf.find('\x1f', pos);
@@ -92,12 +87,23 @@ bool recv_n(int fd, std::string &buf, size_t n, std::vector<std::string> &out) {
         }
         buf.erase(0, pos);
         pos = 0;
-        const ssize_t r = recv(fd, tmp, sizeof tmp, 0);
-        if (r <= 0) return false;
-        buf.append(tmp, (size_t)r);
+        pollfd pf{fd, (short)(POLLIN | (sent < req.size() ? POLLOUT : 0)), 0};
+        if (poll(&pf, 1, 60000) <= 0) return false;
+        if (pf.revents & (POLLERR | POLLHUP | POLLNVAL)) return false;
+        if ((pf.revents & POLLOUT) && sent < req.size()) {
+            const ssize_t w = send(fd, req.data() + sent, req.size() - sent, MSG_NOSIGNAL | MSG_DONTWAIT);
+            if (w < 0 && errno != EAGAIN && errno != EWOULDBLOCK) return false;
+            if (w > 0) sent += (size_t)w;
+        }
+        if (pf.revents & POLLIN) {
+            const ssize_t r = recv(fd, tmp, sizeof tmp, MSG_DONTWAIT);
+            if (r == 0) return false;
+            if (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK) return false;
+            if (r > 0) buf.append(tmp, (size_t)r);
+        }
     }
     buf.erase(0, pos);
-    return true;
+    return sent == req.size();
 }
 
 struct Worker {
@@ -193,7 +199,7 @@ int main(int argc, char **argv) {
                         }
                         me.bytes += o.vlen;
                     }
-                    if (!send_all(fd, req) || !recv_n(fd, buf, b, resp)) {
+                    if (!exchange(fd, req, buf, b, resp)) {
                         failed++;
                         break;
                     }

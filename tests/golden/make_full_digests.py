@@ -12,7 +12,8 @@ compressed members, lengths from the codec) and reports "bitexact"; tests/test_g
 the 200K prefixes through a multi-chunk compress.
 
 Output (data only): tests/golden/full_digests.json
-Usage: python tests/golden/make_full_digests.py [--threads 8]
+Usage: python tests/golden/make_full_digests.py [--threads 8] [--ranks]
+  --ranks: tests/golden/rank_digests.json, the per-rank digests of bench.py --gpus 2/4/8
 """
 import argparse
 import hashlib
@@ -36,10 +37,65 @@ CHECKPOINTS = (4096, 200_000, 1_000_000, 2_000_000, 5_000_000, 10_000_000)
 CHUNK = 250_000
 
 
+# multi-GPU weak scaling (bench.py --gpus N): rank r of N compresses the first RANK_N keys "key"+i whose
+# hashFunc("key"+i) % 128 % N == r (server.cpp:113,121,132), among keys 0 .. route_span - 1
+RANK_WORLDS = (2, 4, 8)
+RANK_N = 10_000_000
+RANK_CHECKPOINTS = (200_000, 1_000_000, 10_000_000)
+
+
+def route_span(n, world):  # = bench.py route_span
+    return int(n * world * 1.05) + 4096
+
+
+def rank_digests(corpus, threads):
+    """Per-rank digests of the north-star workload (10M x 1 KiB JSON slices per GPU) for N = 2, 4, 8."""
+    out = []
+    for world in RANK_WORLDS:
+        route = O.route_keys(0, route_span(RANK_N, world), 128, world)
+        for rank in range(world):
+            t0 = time.time()
+            idx = np.nonzero(route == rank)[0][:RANK_N].astype(np.uint64)
+            assert len(idx) == RANK_N, (world, rank, len(idx))
+            h = hashlib.sha256()
+            gz_bytes = 0
+            marks = {}
+            for first in range(0, RANK_N, CHUNK):
+                m = min(CHUNK, RANK_N - first)
+                vals = O.gen_values_idx(corpus, 0x5EED, 0, idx[first:first + m], 1024)
+                lens, crcs = O.ref_member_records(vals, threads)
+                O.member_records_digest(lens, crcs, h)
+                gz_bytes += int(lens.astype(np.uint64).sum())
+                if first + m in RANK_CHECKPOINTS:
+                    marks[str(first + m)] = {"sha256": h.copy().hexdigest(), "gz_bytes": gz_bytes}
+            out.append({"world": world, "rank": rank, "n": RANK_N, "vlen": 1024, "kind": 0, "seed": 0x5EED,
+                        "index_sha256": hashlib.sha256(idx.astype("<u8").tobytes()).hexdigest(),
+                        "prefixes": marks})
+            print(f"world {world} rank {rank}: {gz_bytes} B, {time.time() - t0:.1f} s", flush=True)
+    doc = {
+        "generator": "tests/golden/make_full_digests.py --ranks",
+        "reference": "/root/reference/src/compressor/gzip_compressor.cpp (built by oracle/Makefile ref)",
+        "zlib_version": O.ref().ref_zlib_version().decode(),
+        "record": "as full_digests.json, over the rank's values in routed-index order",
+        "routing": "rank r of N keeps the first n keys 'key'+i (i = 0 .. route_span - 1, route_span = "
+                   "int(n * N * 1.05) + 4096) with MurmurHash3_x64_128('key'+i, seed 0)[0] % 128 % N == r",
+        "sets": out,
+    }
+    with open(os.path.join(HERE, "rank_digests.json"), "w") as f:
+        json.dump(doc, f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
+    ap.add_argument("--ranks", action="store_true", help="only the per-rank digests (rank_digests.json)")
     args = ap.parse_args()
+    if args.ranks:
+        O.build(ref=True)
+        d = os.path.join(HERE, "data")
+        corpus = b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)) if f.endswith(".json"))
+        rank_digests(corpus, args.threads)
+        return
     O.build(ref=True)
     assert O.ref_available(), "oracle/_ref/libref_gzip.so missing (needs /root/reference)"
     d = os.path.join(HERE, "data")

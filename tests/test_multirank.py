@@ -96,3 +96,30 @@ def test_route_span_covers_every_world():
 
 if __name__ == "__main__":
     sys.exit(pytest.main([__file__, "-q"]))
+
+
+def test_rank_digests_cover_bench_key_selection():
+    """tests/golden/rank_digests.json (the reference's Compress over each rank's routed values,
+    make_full_digests.py --ranks) was computed on exactly the key indices bench.py --gpus N selects:
+    route "key"+i by MurmurHash3 % 128 % N over route_span keys, first n per rank (select_rank_keys)."""
+    import hashlib
+    import json
+    import numpy as np
+    import torch
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "poor-man-s-cache_amd")]
+    import bench
+    from oracle import pyoracle as O
+    with open(os.path.join(ROOT, "tests", "golden", "rank_digests.json")) as f:
+        doc = json.load(f)
+    worlds = sorted({s["world"] for s in doc["sets"]})
+    assert worlds == [2, 4, 8]
+    z = np.load(os.path.join(ROOT, "tests", "golden", "route_golden.npz"))  # the reference's hashFunc
+    for w in worlds:
+        got = O.route_keys(0, int(z["index"].max()) + 1, 128, w)
+        assert all(int(got[i]) == int(h) % 128 % w for i, h in zip(z["index"], z["hash"]))
+        n = doc["sets"][0]["n"]
+        route = torch.from_numpy(O.route_keys(0, bench.route_span(n, w), 128, w))
+        for s in (s for s in doc["sets"] if s["world"] == w):
+            idx = bench.select_rank_keys(route, s["rank"], n).numpy().astype("<u8")
+            assert hashlib.sha256(idx.tobytes()).hexdigest() == s["index_sha256"], (w, s["rank"])
+            assert set(s["prefixes"]) >= {str(n)}
