@@ -610,17 +610,18 @@ struct SmallWave {
     // Resumes a walk cut short by match_all: candidates kPreCand.. of position i, starting
     // from that walk's best / bestq.  Returns the match length (> b0) or 0; *q_out = the
     // nearest candidate achieving it.
+    // `start`: candidates the walk that was cut short already compared (nearest first)
     template <int PK>
     __device__ __forceinline__ uint32_t search(uint32_t i, uint32_t b0, uint32_t len, uint32_t best, uint32_t bestq,
-                               uint32_t *q_out) {
+                               uint32_t *q_out, uint32_t start = kPreCand) {
         const int l = lane_id();
         const uint32_t C = b0 >= 32 ? 1024u : 4096u;
         const uint32_t nice = (len - i) < 258 ? (len - i) : 258;
         const uint32_t wi = load4(i);
         const uint32_t hi = hash3(wi);
         const int r = (int)(PK > 0 ? R[i] & ((1u << (16 - (PK > 0 ? PK : 0))) - 1u) : (uint32_t)R[i]);
-        uint32_t examined = kPreCand;
-        for (int kb = r - 1 - (int)kPreCand;; kb -= 64) {
+        uint32_t examined = start;
+        for (int kb = r - 1 - (int)start;; kb -= 64) {
             const uint32_t thr = best > b0 ? best : b0;
             if (thr >= nice) break; // no candidate can be longer (lengths are capped at nice)
             const uint32_t wthr = thr >= 4 ? load4(i + thr - 3) : 0u;
@@ -882,6 +883,9 @@ struct SmallWave {
         const bool inc = w != 0 && incl <= 64;
         const uint64_t im = ballot(inc); // a prefix of the window's has-candidate offsets
         const uint32_t nl = readlane(incl, 63 - __builtin_clzll(im));
+#ifdef PMC_STAMPS
+        st[7] += nl; // (stamps build: lanes used per eval)
+#endif
         // first lane of each evaluated offset j: offs << 26 | (j + 1) << 19 | R (offs grows
         // with j, so a max-scan hands every lane its owner); other lanes store to dummy slots
         PMC_LDS uint32_t *dmy = EV + 64; // (the u8 mark area, 16 words)
@@ -1087,6 +1091,29 @@ struct SmallWave {
         uint32_t diag_s = 0, diag_s1 = 1, diag_s2 = 2, diag_s3 = 3, diag_v = 0, diag_v1 = 1, diag_v2 = 2, diag_v3 = 3;
 #endif
         uint64_t hcw = rfl64(HC[0]);
+#ifdef PMC_STAMPS
+        // eval usage (stamps build): st[3] evaluated positions, st[4] those the walk consumed,
+        // st[5] evals started inside the previous window's 64-position span
+        uint64_t d_used = 0;
+        uint32_t d_p0 = kNoWindow;
+        auto d_use = [&](uint32_t a, uint32_t b) { // offsets a..b of the current window
+            if (a < 64) d_used |= (b >= 63 ? ~0ull : ((2ull << b) - 1)) & (~0ull << a);
+        };
+        auto d_eval = [&](uint32_t newp0) {
+            if (d_p0 != kNoWindow) {
+                st[3] += (uint64_t)__builtin_popcountll(g.m);
+                st[4] += (uint64_t)__builtin_popcountll(g.m & d_used);
+                st[5] += newp0 - d_p0 < 64 ? 1u : 0u;
+            }
+            d_used = 0;
+            d_p0 = newp0;
+        };
+#define PMC_D_EVAL(x) d_eval(x)
+#define PMC_D_USE(a, b) d_use(a, b)
+#else
+#define PMC_D_EVAL(x)
+#define PMC_D_USE(a, b)
+#endif
         while (i < len) {
             // (the parse state is wave-uniform: keep it in SGPRs so control stays scalar)
             i = rfl(i);
@@ -1146,6 +1173,7 @@ struct SmallWave {
                         i = j;
                         if (i >= len) break;
                         stamp(2);
+                        PMC_D_EVAL(i);
                         eval_group<PK>(g, i, npos, len);
                         stamp(10);
                         count(13);
@@ -1153,6 +1181,7 @@ struct SmallWave {
                     }
                     W = readlane(g.w, (int)off);
                     const uint32_t ty = W >> 30;
+                    PMC_D_USE(off, ty == kStepJump ? (W & 127u) - 1u : (W >> 24) & 63u);
                     if (ty == kStepJump) { // no decision in this window from here: a new one at p0 + b
                         i = g.p0 + (W & 127u);
                         g.p0 = kNoWindow;
@@ -1255,6 +1284,10 @@ struct SmallWave {
                     hcw = rfl64(HC[hci]);
                 }
                 if (sflag((uint32_t)(hcw >> (i & 63)) & 1u)) {
+#ifdef PMC_STAMPS
+                    if (!(i - g.p0 < 64 && ((g.m >> (i - g.p0)) & 1))) PMC_D_EVAL(i);
+                    PMC_D_USE(i - g.p0, i - g.p0);
+#endif
                     const uint32_t e = group_get<PK>(g, i, npos, len);
                     uint32_t m = e & 511, q = (e >> 9) & 0x7fffu;
                     if (e >> 31) {
@@ -2171,7 +2204,7 @@ struct SmallWave {
         PMC_STOP(23, 0)
         PMC_STOP(24, 0)
         PMC_STOP(25, 0)
-        stamp(4);
+        stamp(0); // (the back's times share slot 0: slots 3-5 count the front's eval usage)
         uint64_t nbytes = bitpos >> 3;
         if (l < 8) {
             uint32_t v = l < 4 ? crc : len;
@@ -2189,7 +2222,7 @@ struct SmallWave {
             for (uint64_t k = l; k < nbytes; k += 64) dst[k] = outb[k];
         }
         if (l == 0) *dst_len = (uint32_t)nbytes;
-        stamp(5);
+        stamp(0);
         return 0;
     }
 

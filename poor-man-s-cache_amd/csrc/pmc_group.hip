@@ -101,12 +101,33 @@ PMC_API int pmc_group_route(pmc_group *g, const uint64_t *key_hash, uint32_t num
 }
 
 namespace {
+// Runs fn(lo, hi) over [0, m) on up to `threads` host threads (the calling one included).
+template <class F>
+void par_for(uint32_t m, int threads, F fn) {
+    const uint32_t per = 16384;  // values per thread at least: thread start-up is ~10 us
+    const int t = (int)std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)threads, (m + per - 1) / per));
+    if (t == 1) {
+        fn(0u, m);
+        return;
+    }
+    std::vector<std::thread> th;
+    const uint32_t step = (m + t - 1) / t;
+    for (int k = 1; k < t; k++) {
+        const uint32_t lo = k * step, hi = std::min<uint32_t>(m, lo + step);
+        if (lo < hi) th.emplace_back([=] { fn(lo, hi); });
+    }
+    fn(0u, std::min<uint32_t>(m, step));
+    for (auto &x : th) x.join();
+}
+
 // Member k's share of a group batch: gather its values into pinned memory (back to back), run the
-// pipelined pinned call on its context (slot mode over tiled slots: whole ranges come back), put
-// each output at the caller's dst_off.
+// pipelined pinned call on its context, put each output at the caller's dst_off.  Compress runs in
+// packed mode (only the members' real bytes come back over PCIe, ~0.37 of a 1 KiB value's slot);
+// decompress in slot mode (value sizes are known).  The gather and the scatter are memcpy loops
+// split over `threads` host threads: one thread moving every byte of an 8-GPU batch would bound it.
 int group_share(pmc_group *g, int k, Dir dir, const std::vector<uint32_t> &idx, const uint8_t *src,
                 const uint64_t *src_off, const uint32_t *src_len, uint8_t *dst, const uint64_t *dst_off,
-                const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len) {
+                const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len, int threads) {
     const uint32_t m = (uint32_t)idx.size();
     if (m == 0) return PMC_OK;
     uint64_t in_b = 0, out_b = 0;
@@ -130,20 +151,32 @@ int group_share(pmc_group *g, int k, Dir dir, const std::vector<uint32_t> &idx, 
         const uint32_t i = idx[j];
         soff[j] = so;
         slen[j] = src_len[i];
-        memcpy(s + so, src + src_off[i], src_len[i]);
         so += src_len[i];
         doff[j] = dof;
         dcap[j] = dst_cap[i];
         dof += dst_cap[i];
     }
-    r = pinned_batch(g->ctx[k], dir, s, soff, slen, m, d, doff, dcap, dlen, src_rc, max_len, 0);
+    par_for(m, threads, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t j = lo; j < hi; j++) memcpy(s + soff[j], src + src_off[idx[j]], slen[j]);
+    });
+    const bool packed = dir == kCompress;
+    r = pinned_batch(g->ctx[k], dir, s, soff, slen, m, d, packed ? nullptr : doff, dcap, dlen, src_rc, max_len, 0);
     if (r) return r;
-    for (uint32_t j = 0; j < m; j++) {
-        const uint32_t i = idx[j];
-        rc[i] = src_rc[j];
-        dst_len[i] = dlen[j];
-        if (src_rc[j] == PMC_OK) memcpy(dst + dst_off[i], d + doff[j], dlen[j]);
+    if (packed) {  // member j at the sum of the successful members' lengths before it
+        uint64_t po = 0;
+        for (uint32_t j = 0; j < m; j++) {
+            doff[j] = po;
+            po += src_rc[j] == PMC_OK ? dlen[j] : 0u;
+        }
     }
+    par_for(m, threads, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t j = lo; j < hi; j++) {
+            const uint32_t i = idx[j];
+            rc[i] = src_rc[j];
+            dst_len[i] = dlen[j];
+            if (src_rc[j] == PMC_OK) memcpy(dst + dst_off[i], d + doff[j], dlen[j]);
+        }
+    });
     return PMC_OK;
 }
 
@@ -160,12 +193,17 @@ int group_batch(pmc_group *g, Dir dir, const uint8_t *src, const uint64_t *src_o
     for (uint32_t i = 0; i < n; i++) idx[(key_hash[i] % num_shards) % (uint64_t)G].push_back(i);
     std::vector<int> res(G, PMC_OK);
     std::vector<std::thread> th;
+    // host threads for each member's gather / scatter: the CPUs this process may use, shared out
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    static const int cap = getenv("PMC_GROUP_THREADS") ? atoi(getenv("PMC_GROUP_THREADS")) : 16;
+    const int per = std::max(1, std::min(hw, cap > 0 ? cap : hw) / G);
     for (int k = 1; k < G; k++)
         th.emplace_back([&, k] {
             res[k] = group_share(g, k, dir, idx[k], src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc,
-                                 max_len);
+                                 max_len, per);
         });
-    res[0] = group_share(g, 0, dir, idx[0], src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, max_len);
+    res[0] = group_share(g, 0, dir, idx[0], src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, max_len,
+                         per);
     for (auto &t : th) t.join();
     for (int k = 0; k < G; k++)
         if (res[k]) return res[k];

@@ -15,10 +15,10 @@ import torch  # noqa: E402
 import pmc_codec  # noqa: E402
 from pmc_codec import device as D  # noqa: E402
 
-PHASES = ["stage+crc", "hash+sort", "parse", "trees lit+dist (rest)", "emit", "trailer+copy",
-          "zero+histogram", "#tb_run iters", "#ext iters", "#general steps", "eval", "chain counts", "search", "#groups",
+PHASES = ["stage+crc", "hash+sort", "parse", "#evaluated positions", "#consumed positions", "#evals inside prev span",
+          "zero+histogram", "#eval lanes used", "#ext iters", "#general steps", "eval", "chain counts", "search", "#groups",
           "#parse steps", "#search calls"]
-COUNTS = {7, 8, 9, 13, 14, 15}
+COUNTS = {3, 4, 5, 7, 8, 9, 13, 14, 15}
 IPHASES = ["inf:stage+header", "inf:block hdr+code lens", "inf:table builds", "lane:#decode iters (wave)",
            "lane:#active lane-iters", "lane:prepare", "lane:decode loop", "lane:finish",
            "rec:phase B", "rec:#jump rounds", "rec:#records", "rec:#members"]
