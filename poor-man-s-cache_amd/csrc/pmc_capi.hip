@@ -418,16 +418,26 @@ PMC_API uint32_t pmc_gzip_isize(const void *in, size_t in_len) {
     return p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// Batches of at most this many values, from the host-memory calls (the drop-in's single values, a
+// server's small batches), take the latency path: one wave-per-value kernel that does the whole
+// value (deflate_small_kernel; inflate_kernel for decompress) instead of the throughput pipeline's
+// chain of launches (front, order sort, trees, back; record / lane kernels, CRC verify), which only
+// pays once a batch fills the CUs.
+constexpr uint32_t kLatencyBatch = 64;
+
 static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
                                uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap,
-                               uint32_t *dst_len, int32_t *rc, uint32_t max_len, void *stream) {
+                               uint32_t *dst_len, int32_t *rc, uint32_t max_len, void *stream,
+                               bool latency = false) {
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
     if (max_len == 0) max_len = 1;
     hipStream_t st = (hipStream_t)stream;
-    // src_len[i] > max_len: no variant below claims the value; it gets PMC_E_ARG on the device
-    hipLaunchKernelGGL(arg_check_kernel, dim3((unsigned)std::min<uint64_t>(((uint64_t)n + 255) / 256, 2048)),
-                       dim3(256), 0, st, src_len, (uint64_t)n, (uint64_t)max_len, rc, dst_len);
+    // src_len[i] > max_len: no variant below claims the value; it gets PMC_E_ARG on the device (the
+    // latency path's caller computed max_len from the lengths itself)
+    if (!latency)
+        hipLaunchKernelGGL(arg_check_kernel, dim3((unsigned)std::min<uint64_t>(((uint64_t)n + 255) / 256, 2048)),
+                           dim3(256), 0, st, src_len, (uint64_t)n, (uint64_t)max_len, rc, dst_len);
     DeflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, nullptr,
                   ctx->dbg, -1};
     if (const char *e = getenv("PMC_STOP_AFTER")) a.stop_after = atoi(e); // diagnostic builds only
@@ -437,7 +447,8 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     // kernel with its working set in HBM (pmc_deflate.hip).  PMC_DEFLATE_V1=1 routes everything
     // through the general kernels (A/B and safety net); PMC_DEFLATE_MONO=1 the single-kernel path.
     static const bool force_v1 = getenv("PMC_DEFLATE_V1") && atoi(getenv("PMC_DEFLATE_V1"));
-    static const bool mono = getenv("PMC_DEFLATE_MONO") && atoi(getenv("PMC_DEFLATE_MONO"));
+    static const bool mono_env = getenv("PMC_DEFLATE_MONO") && atoi(getenv("PMC_DEFLATE_MONO"));
+    const bool mono = mono_env || latency;
     static const bool no_big = getenv("PMC_BIG_PASS") && !atoi(getenv("PMC_BIG_PASS"));
     const bool split = !force_v1 && !mono;
     const uint64_t small_lim = force_v1 ? 0 : deflate_small_limit();
@@ -627,11 +638,16 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
 }
 
 static uint64_t inflate_lds_out_limit() { return 48 * 1024; }
+// the output image decompress_batch_body's LDS wave kernel gets for a call with this max_len
+static uint64_t inflate_lds_limit_out(uint64_t max_len) {
+    const uint64_t c = std::min<uint64_t>(inflate_lds_out_limit(), std::max<uint64_t>(max_len, 1));
+    return (c + 63) & ~(uint64_t)63;
+}
 
 static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off,
                                  const uint32_t *src_len, uint32_t n, uint8_t *dst, const uint64_t *dst_off,
                                  const uint32_t *dst_cap, uint32_t *dst_len, int32_t *rc, uint32_t max_len,
-                                 void *stream) {
+                                 void *stream, bool latency = false, bool need_hbm = true) {
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
     hipStream_t st = (hipStream_t)stream;
@@ -641,7 +657,7 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
     // declines (rc = kInflateRetry) goes through the wave-per-member kernels below
     // (PMC_INFLATE_WAVE=1: everything through the wave kernels).
     static const bool wave_only = getenv("PMC_INFLATE_WAVE") && atoi(getenv("PMC_INFLATE_WAVE"));
-    if (!wave_only) {
+    if (!wave_only && !latency) {
         int r = ctx->crcx.ensure((uint64_t)n * 4);
         if (r) return r;
         a.crc_expect = (uint32_t *)ctx->crcx.p;
@@ -725,8 +741,9 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
     }
     // members whose output or input exceeds the LDS image (rare: large values, or garbage
     // input longer than its ISIZE suggests) -> HBM variant; always launched because input
-    // lengths are device-resident (the kernel skips members the LDS kernel handled)
-    {
+    // lengths are device-resident (the kernel skips members the LDS kernel handled) -- unless a
+    // host-memory caller, who knows the lengths, says no member needs it
+    if (need_hbm) {
         uint64_t wb = inflate_wave_bytes(true, 0, 0);
         uint64_t waves = std::min<uint64_t>((uint64_t)ctx->cus * 4, n);
         a.wave_bytes = wb;
@@ -839,20 +856,22 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     if (n == 0) return PMC_OK;
     HostCall guard(ctx);
     HIP_TRY(hipSetDevice(ctx->device));
-    // packed device layout: src bytes back to back, dst slots back to back
-    uint64_t in_bytes = 0, out_bytes = 0, max_len = 0;
+    // packed device layout, in the order of the two copies: [offsets, lengths, caps | source bytes]
+    // go down in one H2D, [output lengths, verdicts | output bytes] come back in one D2H
+    uint64_t in_bytes = 0, out_bytes = 0, max_len = 0, max_in = 0;
     for (uint32_t i = 0; i < n; i++) {
         in_bytes += src_len[i];
         out_bytes += dst_cap[i];
         uint64_t m = dir == kCompress ? src_len[i] : dst_cap[i];
         max_len = std::max(max_len, m);
+        max_in = std::max<uint64_t>(max_in, src_len[i]);
     }
     auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
-    const uint64_t meta = al(n * 8ull) * 2 + al(n * 4ull) * 4;
-    const uint64_t total = meta + al(in_bytes + 16) + al(out_bytes + 16);
-    int r = ctx->pinned.ensure(total);
+    const uint64_t down = al(n * 8ull) * 2 + al(n * 4ull) * 2 + al(in_bytes + 16);
+    const uint64_t up = al(n * 4ull) * 2 + al(out_bytes + 16);
+    int r = ctx->pinned.ensure(down + up);
     if (r) return r;
-    r = ctx->staging.ensure(total);
+    r = ctx->staging.ensure(down + up);
     if (r) return r;
     uint8_t *hp = (uint8_t *)ctx->pinned.p, *dp = (uint8_t *)ctx->staging.p;
     uint64_t o = 0;
@@ -864,12 +883,12 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     o += al(n * 4ull);
     uint32_t *h_dcap = (uint32_t *)(hp + o), *d_dcap = (uint32_t *)(dp + o);
     o += al(n * 4ull);
+    uint8_t *h_src = hp + o, *d_src = dp + o;
+    o += al(in_bytes + 16);
     uint32_t *h_dlen = (uint32_t *)(hp + o), *d_dlen = (uint32_t *)(dp + o);
     o += al(n * 4ull);
     int32_t *h_rc = (int32_t *)(hp + o), *d_rc = (int32_t *)(dp + o);
     o += al(n * 4ull);
-    uint8_t *h_src = hp + o, *d_src = dp + o;
-    o += al(in_bytes + 16);
     uint8_t *h_dst = hp + o, *d_dst = dp + o;
     uint64_t so = 0, doff = 0;
     for (uint32_t i = 0; i < n; i++) {
@@ -882,16 +901,29 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
         doff += dst_cap[i];
     }
     hipStream_t st = ctx->stream;
-    HIP_TRY(hipMemcpyAsync(dp, hp, meta, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(d_src, h_src, in_bytes, hipMemcpyHostToDevice, st));
-    r = dir == kCompress
-            ? pmc_gzip_compress_batch(ctx, d_src, d_soff, d_slen, n, d_dst, d_doff, d_dcap, d_dlen, d_rc,
-                                      (uint32_t)max_len, st)
-            : pmc_gzip_decompress_batch(ctx, d_src, d_soff, d_slen, n, d_dst, d_doff, d_dcap, d_dlen, d_rc,
-                                        (uint32_t)max_len, st);
+    HIP_TRY(hipMemcpyAsync(dp, hp, down, hipMemcpyHostToDevice, st));
+    // (values above the small kernels' limit keep the throughput path: the wave-per-value kernel
+    // that would take them works from HBM and is far slower than the split pipeline's large pass)
+    const bool latency = n <= kLatencyBatch && (dir == kDecompress || max_len <= deflate_small_limit());
+    {
+        const int d = dir == kCompress ? 0 : 1;
+        std::lock_guard<std::recursive_mutex> dir_lock(ctx->dir_mu[d]);
+        r = dir_enter(ctx, d, st);
+        if (!r) {
+            if (dir == kCompress)
+                r = compress_batch_body(ctx, d_src, d_soff, d_slen, n, d_dst, d_doff, d_dcap, d_dlen, d_rc,
+                                        (uint32_t)max_len, st, latency);
+            else  // the wave kernels' HBM variant only for members the LDS image cannot hold
+                r = decompress_batch_body(ctx, d_src, d_soff, d_slen, n, d_dst, d_doff, d_dcap, d_dlen, d_rc,
+                                          (uint32_t)max_len, st, latency,
+                                          !latency || max_len > inflate_lds_limit_out(max_len) ||
+                                              max_in > gzip_bound(inflate_lds_limit_out(max_len)) + 64);
+            const int r2 = dir_leave(ctx, d, st);
+            if (!r) r = r2;
+        }
+    }
     if (r) return r;
-    HIP_TRY(hipMemcpyAsync(h_dlen, d_dlen, al(n * 4ull) * 2, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(h_dst, d_dst, out_bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h_dlen, d_dlen, up, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     uint64_t po = 0;
     for (uint32_t i = 0; i < n; i++) {

@@ -828,7 +828,6 @@ struct SmallWave {
         uint64_t fast; // evaluated, usable, not cut, and position + 1 does not improve on it
         uint64_t impr; // evaluated, usable, not cut, < 258, and position + 1 improves on it
         uint64_t cut;  // evaluated, walk cut short (search() decides)
-#ifndef PMC_WALK_V1
         // Step records (lane o): the outcome of a fresh-state walk entering the window at offset
         // o, so a walk step is two v_readlane and one scalar branch instead of the mask shifts and
         // find-first-sets of the stop / cut / impr / fast tests on the scalar unit.
@@ -836,7 +835,6 @@ struct SmallWave {
         //       length and source the walk reads from e; CUT: pos = the stop; JUMP: b = the
         //       offset to continue from, 0..64)
         uint32_t w;
-#endif
     };
     static constexpr uint32_t kStepJump = 0, kStepCut = 1, kStepPend = 2, kStepFast = 3;
     static constexpr uint32_t kNoWindow = 0x80000000u; // a p0 no position reaches (i - p0 >= 64)
@@ -963,7 +961,6 @@ struct SmallWave {
         g.fast = ballot((okfast & no_impr) != 0u);
         g.impr = ballot((okfast & impr) != 0u);
         g.cut = ballot((ev & cutc) != 0u);
-#ifndef PMC_WALK_V1
         // step record of lane l (vector ALU; the masks are uniform): the first stop sj >= l, and
         // from a usable sj the end st of its run of lazy improvements (impr bit 63 is clear)
         const uint64_t sx = g.stop & (~0ull << l);
@@ -974,7 +971,6 @@ struct SmallWave {
         const uint32_t ty = evs ? (cts ? kStepCut : fst ? kStepFast : kStepPend) : kStepJump;
         const uint32_t pos = cts ? sjc : st;
         g.w = ty << 30 | pos << 24 | sj;
-#endif
     }
     // Token sink: tokens collect in one VGPR (lane k holds token 64 * block + k) and leave
     // with one coalesced store per 64 tokens, so emitting costs no exec-masked stores.
@@ -983,20 +979,12 @@ struct SmallWave {
     };
     __device__ void tb_flush(TokBuf &t) { tok[t.n - 64 + (uint32_t)lane_id()] = t.v; }
     __device__ void tb_put(TokBuf &t, uint32_t x) {
-#ifdef PMC_DIAG_NOTOK // diagnostic: count tokens only (output invalid; measures emission cost)
-        t.n++;
-        return;
-#endif
         t.v = (uint32_t)lane_id() == (t.n & 63) ? x : t.v;
         t.n++;
         if ((t.n & 63) == 0) tb_flush(t);
     }
     // literal tokens for positions p .. p + cnt - 1
     __device__ void tb_run(TokBuf &t, uint32_t p, uint32_t cnt) {
-#ifdef PMC_DIAG_NOTOK
-        t.n += cnt;
-        return;
-#endif
         const uint32_t l = (uint32_t)lane_id();
         while (cnt) {
             count(7);
@@ -1018,7 +1006,6 @@ struct SmallWave {
     // [lf, len) goes out at the end -- no per-literal bookkeeping on the scalar unit.
     __device__ void tb_match(TokBuf &t, uint32_t lf, uint32_t s, uint32_t m) {
         const uint32_t l = (uint32_t)lane_id(), nl = s - lf, cnt = nl + 1;
-#if !defined(PMC_DIAG_NOTOK) && !defined(PMC_WALK_V1)
         // first 64 tokens with every lane storing (no exec mask work on the scalar unit): lanes
         // past the run repeat the match token at its own slot, so no byte past it is written
         {
@@ -1031,22 +1018,14 @@ struct SmallWave {
                 if (k < cnt) tok[t.n + k] = k < nl ? lf + k : m;
             }
         }
-#elif !defined(PMC_DIAG_NOTOK)
-        for (uint32_t b = 0; b < cnt; b += 64) {
-            const uint32_t k = b + l;
-            if (k < cnt) tok[t.n + k] = k < nl ? lf + k : m;
-        }
-#endif
         t.n += cnt;
     }
     __device__ void tb_lits(TokBuf &t, uint32_t lf, uint32_t e) {
         const uint32_t l = (uint32_t)lane_id(), cnt = e - lf;
-#ifndef PMC_DIAG_NOTOK
         for (uint32_t b = 0; b < cnt; b += 64) {
             const uint32_t k = b + l;
             if (k < cnt) tok[t.n + k] = lf + k;
         }
-#endif
         t.n += cnt;
     }
     // longest_match record of has-candidate position x (evaluating a new window if needed)
@@ -1087,9 +1066,6 @@ struct SmallWave {
         TokBuf tb;
         uint32_t i = 0, ml = 2, ms = 0, lf = 0; // lf: first position of the pending literal run
         uint32_t hci = 0;              // HC word cached in SGPRs
-#if defined(PMC_DIAG_SALU) || defined(PMC_DIAG_VALU)
-        uint32_t diag_s = 0, diag_s1 = 1, diag_s2 = 2, diag_s3 = 3, diag_v = 0, diag_v1 = 1, diag_v2 = 2, diag_v3 = 3;
-#endif
         uint64_t hcw = rfl64(HC[0]);
 #ifdef PMC_STAMPS
         // eval usage (stamps build): st[3] evaluated positions, st[4] those the walk consumed,
@@ -1122,28 +1098,6 @@ struct SmallWave {
             lf = rfl(lf);
             tb.n = rfl(tb.n);
             count(14);
-#ifdef PMC_DIAG_SALU // diagnostic builds only: extra scalar / vector work per parse step
-            // (s_mov_b32 / v_mov_b32 on independent registers: no SCC or VCC side effects)
-            asm volatile("s_mov_b32 %0, %1\n s_mov_b32 %1, %2\n s_mov_b32 %2, %3\n s_mov_b32 %3, %0\n"
-                         "s_mov_b32 %0, %1\n s_mov_b32 %1, %2\n s_mov_b32 %2, %3\n s_mov_b32 %3, %0\n"
-                         "s_mov_b32 %0, %1\n s_mov_b32 %1, %2\n s_mov_b32 %2, %3\n s_mov_b32 %3, %0\n"
-                         "s_mov_b32 %0, %1\n s_mov_b32 %1, %2\n s_mov_b32 %2, %3\n s_mov_b32 %3, %0\n"
-                         "s_mov_b32 %0, %1\n s_mov_b32 %1, %2\n s_mov_b32 %2, %3\n s_mov_b32 %3, %0\n"
-                         : "+s"(diag_s), "+s"(diag_s1), "+s"(diag_s2), "+s"(diag_s3));
-#endif
-#ifdef PMC_DIAG_NOP
-            asm volatile("s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n"
-                         "s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n s_nop 0\n");
-#endif
-#ifdef PMC_DIAG_VALU
-            asm volatile("v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
-                         "v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
-                         "v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
-                         "v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
-                         "v_mov_b32 %0, %1\n v_mov_b32 %1, %2\n v_mov_b32 %2, %3\n v_mov_b32 %3, %0\n"
-                         : "+v"(diag_v), "+v"(diag_v1), "+v"(diag_v2), "+v"(diag_v3));
-#endif
-#ifndef PMC_WALK_V1
             if (ml == 2) {
                 // Fresh state.  Inside the current window the step record of offset i - p0 holds
                 // the whole step (positions without candidates are never stops, so no HC scan is
@@ -1207,74 +1161,6 @@ struct SmallWave {
                 }
                 i = ps; // a cut walk: the general step decides
             }
-#else
-            if (ml == 2) {
-                // no pending match: positions without chain candidates only pass the pending
-                // literal on, so jump to the next position that has candidates
-                uint32_t j = len;
-                uint32_t w = i >> 6;
-                if (w < nw) {
-                    if (w != hci) {
-                        hci = w;
-                        hcw = rfl64(HC[w]);
-                    }
-                    uint64_t m = hcw & (~0ull << (i & 63));
-                    while (!m && ++w < nw) {
-                        hci = w;
-                        hcw = rfl64(HC[w]);
-                        m = hcw;
-                    }
-                    if (m) j = w * 64 + (uint32_t)__builtin_ctzll(m);
-                }
-                // (j >= i; literals up to j stay implied.  Unconditional updates and single integer
-                // tests keep each branch one s_cmp: bool values merged across blocks became lane-mask
-                // selects on the scalar unit this kernel saturates)
-                i = j;
-                if (i >= len) break;
-                // Window walk from a fresh state at has-candidate position i (< npos): in the
-                // evaluated window, unusable results pass as literals and a usable one that
-                // position + 1 does not improve on is emitted at once (eval_group's stop / fast
-                // masks), so one step covers a literal run and its match.  Cut walks and lazy
-                // improvements take the general step below; an unevaluated position with
-                // candidates starts a new window.
-                uint32_t off = i - g.p0;
-                const uint32_t inwin = sflag((uint32_t)(g.m >> (off & 63)) & (off < 64 ? 1u : 0u));
-                if (!inwin) {
-                    stamp(2);
-                    eval_group<PK>(g, i, npos, len);
-                    stamp(10);
-                    count(13);
-                    off = 0;
-                }
-                const uint64_t sm = g.stop >> off;
-                if (!sm) { // literals to the window's end
-                    i = g.p0 + 64 < len ? g.p0 + 64 : len;
-                    continue;
-                }
-                const uint32_t sj = off + (uint32_t)__builtin_ctzll(sm), js = g.p0 + sj;
-                i = js;                               // (js >= i)
-                if (!sflag((uint32_t)(g.m >> sj) & 1u)) continue; // unevaluated: new window at js
-                if (!sflag((uint32_t)(g.cut >> sj) & 1u)) {
-                    // usable at js: the run of lazy improvements js, js + 1, ... ends at t (bit
-                    // 63 of impr is always clear); positions js .. t - 1 become literals
-                    const uint32_t st = sj + (uint32_t)__builtin_ctzll(~(g.impr >> sj)), t = g.p0 + st;
-                    const uint32_t e0 = readlane(g.e, (int)st);
-                    const uint32_t b0 = e0 & 511, q0 = (e0 >> 9) & 0x7fffu;
-                    if (sflag((uint32_t)(g.fast >> st) & 1u)) {
-                        tb_match(tb, lf, t, ((t - q0) << 16) | (b0 - 3));
-                        i = t + b0;
-                        lf = i;
-                        continue;
-                    }
-                    // whether t + 1 improves is not known here (cut or unevaluated): the general
-                    // step continues at t + 1 with t's match pending
-                    i = t + 1;
-                    ml = b0;
-                    ms = q0;
-                    continue;
-                }
-            }
-#endif
             count(9);
             const uint32_t pl = ml, pm = ms;
             ml = 2;
@@ -1315,10 +1201,6 @@ struct SmallWave {
             }
         }
         tb_lits(tb, lf, len);
-#if defined(PMC_DIAG_SALU) || defined(PMC_DIAG_VALU)
-        if (rfl(diag_s + diag_s1 + diag_s2 + diag_s3 + diag_v + diag_v1 + diag_v2 + diag_v3) == 0xdeadbeefu)
-            tb_lits(tb, 0, 1); // (keeps the diagnostic work alive)
-#endif
         wave_sync_global();
         return rfl(tb.n);
     }

@@ -34,7 +34,7 @@ def main():
     assert ctx, "no device"
     R = O.ref() if O.ref_available() else None
     out = {"note": __doc__.split("\n\n")[1].replace("\n", " "), "sizes": []}
-    for vlen in (256, 1024, 4096, 30000):
+    for vlen in (32, 256, 1024, 4096, 30000):
         n = args.calls if vlen <= 4096 else max(200, args.calls // 5)
         vals = [v.tobytes() for v in O.gen_values(corpus, 0x5EED, 0, 0, n, vlen)]
         cap = pmc_codec.gzip_bound(vlen)

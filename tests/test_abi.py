@@ -79,10 +79,14 @@ def test_host_key_hash_matches_reference_hash():
     for i, h in zip(z["index"], z["hash"]):
         k = b"key%d" % int(i)
         assert L.pmc_key_hash(k, len(k)) == int(h), int(i)
-    # every tail length 0..15 and a few full blocks, against the oracle's restatement
+    # keys of every length 0..70 -- the 16-byte block loop and every tail length, bytes up to 0xff --
+    # against the reference's hashFunc too (make_route_golden.py), and the oracle's restatement
     from oracle import pyoracle as O
     O.lib().oracle_murmur3_x64_128_h1.restype = ctypes.c_uint64
     O.lib().oracle_murmur3_x64_128_h1.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32]
-    for n in range(0, 70):
-        k = bytes((7 * j + 3) % 251 + 1 for j in range(n))
-        assert L.pmc_key_hash(k, n) == O.lib().oracle_murmur3_x64_128_h1(k, n, 0), n
+    blob, off, kh = z["key_blob"].tobytes(), z["key_off"], z["key_hash"]
+    assert {int(off[i + 1] - off[i]) for i in range(len(kh))} == set(range(71))
+    for i in range(len(kh)):
+        k = blob[int(off[i]):int(off[i + 1])]
+        assert L.pmc_key_hash(k, len(k)) == int(kh[i]), (len(k), k)
+        assert O.lib().oracle_murmur3_x64_128_h1(k, len(k), 0) == int(kh[i]), (len(k), k)
