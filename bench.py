@@ -480,6 +480,22 @@ def main():
                     tsrc = os.path.relpath(args.traffic, ROOT)
             except (OSError, ValueError):
                 traffic = None
+        # issue floors of the dominant kernel from its counters (when measured on these sources): a wave64
+        # VALU instruction occupies its SIMD 2 cycles (4 SIMDs per CU), a scalar instruction the CU's one
+        # scalar unit 1 cycle; the clock is the measured GRBM_GUI_ACTIVE / 8 XCDs over the launch time
+        floors = None
+        if issue and issue.get("counters_per_launch"):
+            cp = issue["counters_per_launch"]
+            per_launch_vals = n / dom_launches
+            clk_hz = cp["GRBM_GUI_ACTIVE"] / 8.0 / avg_launch_s
+            cus = 256
+            floors = {"valu_per_value": cp["SQ_INSTS_VALU"] / per_launch_vals,
+                      "salu_per_value": cp["SQ_INSTS_SALU"] / per_launch_vals,
+                      "clock_ghz": clk_hz / 1e9,
+                      "valu_floor_ms": cp["SQ_INSTS_VALU"] * 2.0 / (4 * cus) / clk_hz * 1e3,
+                      "salu_floor_ms": cp["SQ_INSTS_SALU"] / cus / clk_hz * 1e3,
+                      "note": "per launch; VALU: 2 cycles per wave64 instruction on each of 4 SIMDs per CU, "
+                              "SALU: one scalar unit per CU"}
         out = {
             "metric": METRIC, "value": gib / t_step_s, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": t_step_s * 1e3, "higher_is_better": True, "scaling": "weak",
@@ -494,7 +510,11 @@ def main():
                        "parallelism": f"shard-partitioned x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-                         "issue": issue,
+                         "issue": issue, "issue_floors": floors,
+                         # the whole step (compress + decompress) against the same peak
+                         "path": {"alg_bytes_per_step": alg_c + alg_d,
+                                  "achieved": (alg_c + alg_d) / (tc + td) / 1e9,
+                                  "frac": (alg_c + alg_d) / (tc + td) / 1e9 / HBM_PEAK_GBS},
                          "kernel": pmc_codec.KERNEL_NAMES[dom],
                          "alg_bytes_per_launch": alg_launch, "avg_launch_ms": avg_launch_s * 1e3,
                          "launches_per_step": dom_launches,

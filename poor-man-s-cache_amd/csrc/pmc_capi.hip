@@ -135,13 +135,14 @@ struct DevBuf {
 struct HostBuf {
     void *p = nullptr;
     size_t cap = 0;
+    unsigned flags = hipHostMallocDefault;
     int ensure(size_t n) {
         if (n <= cap) return PMC_OK;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
         size_t want = std::max(n, (size_t)4096);
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&p, want, flags);
         if (e != hipSuccess) {
             set_err("hipHostMalloc", e);
             return PMC_Z_MEM_ERROR;
@@ -191,6 +192,8 @@ struct pmc_ctx {
     DevBuf staging;              // device side of host-API calls
     uint64_t *dbg = nullptr;     // diagnostic stamp sums (PMC_STAMPS builds)
     HostBuf pinned;              // host side of host-API calls
+    HostBuf zc;                  // latency path: coherent host memory the kernel reads and writes in place
+    void *zc_dev = nullptr;      // its device address
     // pmc_gzip_*_batch_pinned: chunk c's H2D (stream h2d), kernels (stream) and D2H (stream d2h)
     // overlap those of chunks c +- 1; slot c & 1 of `pipe` holds chunk c's arrays and bytes.
     struct Pipe {
@@ -383,6 +386,7 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     c->krecs.clear();
     c->staging.release();
     c->pinned.release();
+    c->zc.release();
     if (c->pipe.h2d) {
         (void)hipStreamSynchronize(c->pipe.d2h);
         for (int k = 0; k < 2; k++) {
@@ -869,11 +873,32 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
     const uint64_t down = al(n * 8ull) * 2 + al(n * 4ull) * 2 + al(in_bytes + 16);
     const uint64_t up = al(n * 4ull) * 2 + al(out_bytes + 16);
-    int r = ctx->pinned.ensure(down + up);
-    if (r) return r;
-    r = ctx->staging.ensure(down + up);
-    if (r) return r;
-    uint8_t *hp = (uint8_t *)ctx->pinned.p, *dp = (uint8_t *)ctx->staging.p;
+    // (values above the small kernels' limit keep the throughput path: the wave-per-value kernel
+    // that would take them works from HBM and is far slower than the split pipeline's large pass)
+    const bool latency = n <= kLatencyBatch && (dir == kDecompress || max_len <= deflate_small_limit());
+    // The latency path's kernel reads its inputs from, and writes its outputs to, coherent host memory in
+    // place: no H2D / D2H copies (each a runtime copy kernel of its own) around its one launch.
+    // PMC_LAT_COPY=1 stages them through device memory instead (A/B).
+    static const bool lat_copy = getenv("PMC_LAT_COPY") && atoi(getenv("PMC_LAT_COPY"));
+    const bool zc = latency && !lat_copy;
+    uint8_t *hp, *dp;
+    int r;
+    if (zc) {
+        ctx->zc.flags = hipHostMallocCoherent;
+        const void *old = ctx->zc.p;
+        r = ctx->zc.ensure(down + up);
+        if (r) return r;
+        if (ctx->zc.p != old) HIP_TRY(hipHostGetDevicePointer(&ctx->zc_dev, ctx->zc.p, 0));
+        hp = (uint8_t *)ctx->zc.p;
+        dp = (uint8_t *)ctx->zc_dev;
+    } else {
+        r = ctx->pinned.ensure(down + up);
+        if (r) return r;
+        r = ctx->staging.ensure(down + up);
+        if (r) return r;
+        hp = (uint8_t *)ctx->pinned.p;
+        dp = (uint8_t *)ctx->staging.p;
+    }
     uint64_t o = 0;
     uint64_t *h_soff = (uint64_t *)(hp + o), *d_soff = (uint64_t *)(dp + o);
     o += al(n * 8ull);
@@ -901,10 +926,7 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
         doff += dst_cap[i];
     }
     hipStream_t st = ctx->stream;
-    HIP_TRY(hipMemcpyAsync(dp, hp, down, hipMemcpyHostToDevice, st));
-    // (values above the small kernels' limit keep the throughput path: the wave-per-value kernel
-    // that would take them works from HBM and is far slower than the split pipeline's large pass)
-    const bool latency = n <= kLatencyBatch && (dir == kDecompress || max_len <= deflate_small_limit());
+    if (!zc) HIP_TRY(hipMemcpyAsync(dp, hp, down, hipMemcpyHostToDevice, st));
     {
         const int d = dir == kCompress ? 0 : 1;
         std::lock_guard<std::recursive_mutex> dir_lock(ctx->dir_mu[d]);
@@ -923,7 +945,7 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
         }
     }
     if (r) return r;
-    HIP_TRY(hipMemcpyAsync(h_dlen, d_dlen, up, hipMemcpyDeviceToHost, st));
+    if (!zc) HIP_TRY(hipMemcpyAsync(h_dlen, d_dlen, up, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     uint64_t po = 0;
     for (uint32_t i = 0; i < n; i++) {

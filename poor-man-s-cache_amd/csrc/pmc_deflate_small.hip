@@ -922,11 +922,13 @@ struct SmallWave {
         uint32_t off = 16;
         while (ballot(ext != 0u)) {
             count(8);
+            // (lane masks, not products with ext: a 32-bit multiply is a quarter-rate VALU op)
+            const uint32_t xm = 0u - ext;
             uint64_t C0, C1, D0, D1;
-            load16((P + off) * ext, C0, C1);
-            load16((q + off) * ext, D0, D1);
+            load16((P + off) & xm, C0, C1);
+            load16((q + off) & xm, D0, D1);
             const uint64_t z0 = C0 ^ D0, z1 = C1 ^ D1;
-            cl += ext * (off + eq16(z0, z1) - cl);
+            cl = ((off + eq16(z0, z1)) & xm) | (cl & ~xm);
             ext &= is0(z0, z1) & ((off + 16u - nice) >> 31);
             off += 16;
         }
@@ -1396,15 +1398,19 @@ struct SmallWave {
     }
 
     // per maximal run of code lengths (value v, length R): bl-code counts (scan_tree)
+    // R / 6 and R / 138 for run lengths R <= 288 by 24-bit multiplies (full-rate VALU ops; the
+    // compiler's reciprocal divisions used quarter-rate 32-bit ones): exact for R < 32768 / 527
+    __device__ static uint32_t div6(uint32_t x) { return __umul24(x, 10923u) >> 16; }
+    __device__ static uint32_t div138(uint32_t x) { return __umul24(x, 475u) >> 16; }
     __device__ static void run_counts(uint32_t v, uint32_t R, PMC_LDS uint32_t *blfreq) {
         if (v) {
-            uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = rem / 6, last = rem % 6;
+            uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = div6(rem), last = rem - __umul24(full, 6u);
             uint32_t nv = (c1 < 4 ? c1 : 1) + (last < 3 ? last : 0);
             uint32_t n16 = (c1 >= 4 ? 1 : 0) + full + (last >= 3 ? 1 : 0);
             if (nv) lds_add(&blfreq[v], nv);
             if (n16) lds_add(&blfreq[16], n16);
         } else {
-            uint32_t full = R / 138, last = R % 138;
+            uint32_t full = div138(R), last = R - __umul24(full, 138u);
             uint32_t n18 = full + (last > 10 ? 1 : 0), n17 = (last >= 3 && last <= 10) ? 1 : 0;
             uint32_t n0 = last < 3 ? last : 0;
             if (n0) lds_add(&blfreq[0], n0);
@@ -1417,15 +1423,15 @@ struct SmallWave {
         const uint32_t Lv = blcode[v] >> 16;
         if (v) {
             const uint32_t L16 = (blcode[16] >> 16) + 2;
-            const uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = rem / 6, last = rem % 6;
-            uint32_t n = c1 < 4 ? c1 * Lv : Lv + L16;
-            n += full * L16;
-            n += last ? (last < 3 ? last * Lv : L16) : 0u;
+            const uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = div6(rem), last = rem - __umul24(full, 6u);
+            uint32_t n = c1 < 4 ? __umul24(c1, Lv) : Lv + L16;
+            n += __umul24(full, L16);
+            n += last ? (last < 3 ? __umul24(last, Lv) : L16) : 0u;
             return n;
         }
         const uint32_t L17 = (blcode[17] >> 16) + 3, L18 = (blcode[18] >> 16) + 7;
-        const uint32_t full = R / 138, last = R % 138;
-        return full * L18 + (last ? (last < 3 ? last * Lv : last <= 10 ? L17 : L18) : 0u);
+        const uint32_t full = div138(R), last = R - __umul24(full, 138u);
+        return __umul24(full, L18) + (last ? (last < 3 ? __umul24(last, Lv) : last <= 10 ? L17 : L18) : 0u);
     }
     // bits of one run (send_tree); emit into the image at pos when write (the run's codes are
     // gathered in a 64-bit register and ORed into the image a register at a time)
@@ -1447,7 +1453,7 @@ struct SmallWave {
         };
         uint32_t acc = 0;
         if (v) {
-            uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = rem / 6, last = rem % 6;
+            uint32_t c1 = R < 7 ? R : 7, rem = R - c1, full = div6(rem), last = rem - __umul24(full, 6u);
             if (c1 < 4) {
                 for (uint32_t k = 0; k < c1; k++) put(v, 0, 0, acc);
             } else {
@@ -1463,7 +1469,7 @@ struct SmallWave {
                 }
             }
         } else {
-            uint32_t full = R / 138, last = R % 138;
+            uint32_t full = div138(R), last = R - __umul24(full, 138u);
             for (uint32_t k = 0; k < full; k++) put(18, 127, 7, acc);
             if (last) {
                 if (last < 3) {

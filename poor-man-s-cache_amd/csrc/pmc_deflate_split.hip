@@ -134,7 +134,9 @@ struct LaneTrees {
         return kind == 1 ? 5u : x < 144 ? 8u : x < 256 ? 9u : x < 280 ? 7u : 8u;
     }
     template <class Freq>
-    __device__ int build(Freq freq, int elems, uint32_t row0, int kind, int max_length, int64_t &opt, int64_t &stat,
+    // (opt / stat: bit counts of one value's block, < 2^32; 32-bit sums of 24-bit products are full-rate
+    // VALU ops, 64-bit multiply-adds quarter-rate ones)
+    __device__ int build(Freq freq, int elems, uint32_t row0, int kind, int max_length, uint32_t &opt, uint32_t &stat,
                          PMC_GLB const uint16_t *grow = nullptr) {
         int heap_len = 0, max_code = -1;
         if (grow) {
@@ -253,8 +255,8 @@ struct LaneTrees {
                         blc[bits * 64]++;
                         const uint32_t f = key >> 15;
                         const uint32_t xb = xbits(kind, x);
-                        opt += (int64_t)f * (bits + xb);
-                        if (kind != 2) stat += (int64_t)f * (static_len(kind, x) + xb);
+                        opt += __umul24(f, bits + xb);
+                        if (kind != 2) stat += __umul24(f, static_len(kind, x) + xb);
                     }
                 }
             }
@@ -281,7 +283,7 @@ struct LaneTrees {
                     if (x >= (uint32_t)elems) continue;
                     const uint32_t cur = lens[row0 + x];
                     if (cur != (uint32_t)bits) {
-                        opt += ((int64_t)bits - (int64_t)cur) * (int64_t)(key >> 15);
+                        opt += (uint32_t)((int32_t)bits - (int32_t)cur) * (key >> 15);
                         lens[row0 + x] = (uint8_t)bits;
                     }
                     n--;
@@ -344,7 +346,7 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC
     t.lens = a.cL + v * kSplitRows;
     t.mg = a.cG + ((slot >> 6) * kMergeRows) * 64 + (slot & 63); // (by lane slot: coalesced)
     for (uint32_t s = 0; s < kSplitRows; s += 16) *reinterpret_cast<uint4 *>(t.lens + s) = make_uint4(0, 0, 0, 0);
-    int64_t opt = 0, stat = 0;
+    uint32_t opt = 0, stat = 0;
     auto hist = [&](int s) -> uint32_t { return t.hist[s]; };
     const int l_max = t.build(hist, kLCodes, 0, 0, kMaxBits, opt, stat, (PMC_GLB const uint16_t *)t.hist);
     if (t.deferred) {
@@ -362,9 +364,9 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC
     int mbi;
     for (mbi = kBLCodes - 1; mbi >= 3; mbi--)
         if (t.lens[kLCodes + kDCodes + bl_order_cf(mbi)] != 0) break;
-    opt += 3 * ((int64_t)mbi + 1) + 5 + 5 + 4;
-    uint32_t opt_lenb = (uint32_t)(((uint64_t)opt + 3 + 7) >> 3);
-    const uint32_t static_lenb = (uint32_t)(((uint64_t)stat + 3 + 7) >> 3);
+    opt += 3 * ((uint32_t)mbi + 1) + 5 + 5 + 4;
+    uint32_t opt_lenb = (opt + 3 + 7) >> 3;
+    const uint32_t static_lenb = (stat + 3 + 7) >> 3;
     if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
     const uint32_t type = len + 4 <= opt_lenb ? 0u : static_lenb == opt_lenb ? 1u : 2u;
     a.cP[v] = type | (uint32_t)l_max << 2 | (uint32_t)d_max << 11 | (uint32_t)mbi << 16;
