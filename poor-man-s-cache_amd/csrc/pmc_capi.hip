@@ -716,12 +716,19 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
                     [&] { hipLaunchKernelGGL(inflate_rec_kernel, dim3(rb), dim3(64), kRecLdsBytes, st, a); });
             a.big_only = 1;
         }
-        klaunch(ctx, PMC_K_INFLATE_LANE, st,
-                [&] { hipLaunchKernelGGL(inflate_lane_kernel, dim3(lb), dim3(64), kLaneLdsBytes, st, a); });
+        klaunch(ctx, PMC_K_INFLATE_LANE, st, [&] {
+            hipLaunchKernelGGL(inflate_lane_kernel<kLaneLitCap>, dim3(lb), dim3(64), kLaneLdsBytes, st, a);
+            // members whose lit/len code did not fit its lists (a third of 30 KB JSON values): the wide
+            // instance (it skips every other member at once)
+            hipLaunchKernelGGL(inflate_lane_kernel<kLaneWideLit>, dim3(lb), dim3(64), kLaneWideLdsBytes, st, a);
+        });
         a.big_only = 0;
+        static const int diag_stop = getenv("PMC_DIAG_INFLATE_STOP") ? atoi(getenv("PMC_DIAG_INFLATE_STOP")) : 0;
+        if (diag_stop == 1) return PMC_OK; // (diagnostic: verdicts of the lane kernels, unverified)
         const unsigned vb = (unsigned)std::min<uint64_t>(((uint64_t)n + 511) / 512, (uint64_t)ctx->cus * 4);
         klaunch(ctx, PMC_K_INFLATE_VERIFY, st,
                 [&] { hipLaunchKernelGGL(inflate_verify_kernel, dim3(vb), dim3(512), 0, st, a); });
+        if (diag_stop == 2) return PMC_OK; // (diagnostic: verdicts after the CRC check)
         a.retry_only = 1;
         a.order = nullptr;
     }

@@ -27,6 +27,9 @@
 namespace pmc {
 
 constexpr int kLaneLitCap = 96, kLaneDistCap = 30;
+// the wide instance's lit/len lists: members declined only because their lit/len code uses more than 96
+// symbols (a third of 30 KB JSON members, up to ~110) take a second pass at 3 waves per CU
+constexpr int kLaneWideLit = 128;
 // per-lane LDS columns (u16 words, entry i of lane l at word i * 64 + l).  Decode-time:
 // symbol lists and bases.  Build-time scratch (counts / offsets, code-length code) lives in
 // the output ring's bytes, which are only written once decoding starts.
@@ -56,9 +59,16 @@ constexpr uint32_t kWinDw = PMC_LANE_WIN, kWinHalf = kWinDw / 2;
 // output ring per lane (bytes; flushed by halves); matches reaching further back than
 // kRing - 16 read dst (L2).  (128 fits five waves per CU but measured slower than 256 at four.)
 constexpr uint32_t kRing = PMC_LANE_RING, kFlush = kRing / 2;
-constexpr uint32_t kLaneRingOff = (uint32_t)kColWords * 64 * 2;            // output rings (LaneOut)
-constexpr uint32_t kLaneWinOff = kLaneRingOff + kRing / 4 * 64 * 4;        // input windows (LaneWin)
-constexpr uint32_t kLaneLdsBytes = kLaneWinOff + kWinDw * 64 * 4;
+// the lane kernel's LDS per 64-lane block for lit/len lists of LIT entries: columns | rings | windows
+template <int LIT>
+struct LaneLayout {
+    typedef LaneCols<LIT, kLaneDistCap> Cols;
+    static constexpr uint32_t kRingOff = (uint32_t)Cols::kColWords * 64 * 2; // output rings (LaneOut)
+    static constexpr uint32_t kWinOff = kRingOff + kRing / 4 * 64 * 4;       // input windows (LaneWin)
+    static constexpr uint32_t kLds = kWinOff + kWinDw * 64 * 4;
+};
+constexpr uint32_t kLaneLdsBytes = LaneLayout<kLaneLitCap>::kLds;
+constexpr uint32_t kLaneWideLdsBytes = LaneLayout<kLaneWideLit>::kLds;
 static_assert((kBColCl + 19) * 64 <= kRing * 64, "build columns live in the output rings");
 
 // 16-byte load through a global (not flat) pointer: flat loads also count against lgkmcnt,
@@ -348,9 +358,11 @@ __device__ bool lane_lengths(LaneIn &in, const LaneClc &clc, uint32_t nlen, uint
 // Header and block header of a single-block fixed/dynamic member, code tables built;
 // false = decline (stored or multi-block members, header flags, malformed codes ...).  *over
 // (if given) is set when the only reason is C's list capacity: the lane kernel's lists hold it.
+// (wide_lit / wide_dist: the capacity *over tests against)
 template <class C>
 __device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
-                             LaneCode<15> &dist, bool &fixed, bool *over = nullptr) {
+                             LaneCode<15> &dist, bool &fixed, bool *over = nullptr, int wide_lit = kLaneLitCap,
+                             int wide_dist = kLaneDistCap) {
     if (in.len < 18) return false;
     if (in.byte_at(0) != 0x1f || in.byte_at(1) != 0x8b || in.byte_at(2) != 8 || in.byte_at(3) != 0) return false;
     in.seek(80);
@@ -403,7 +415,7 @@ __device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t 
         nd += bcol[(kBColCntD + L) * 64];
     }
     if (nl > (uint32_t)C::kLit || nd > (uint32_t)C::kDist) {
-        if (over) *over = nl <= (uint32_t)kLaneLitCap && nd <= (uint32_t)kLaneDistCap;
+        if (over) *over = nl <= (uint32_t)wide_lit && nd <= (uint32_t)wide_dist;
         return false;
     }
     if (!lit.build(bcol + kBColCntL * 64) || !dist.build(bcol + kBColCntD * 64)) return false;
@@ -475,19 +487,27 @@ struct LaneOut {
     }
 };
 
+// LIT = kLaneLitCap: every member (a.big_only: those the record kernel marked kInflateBig); a member
+// declined only for its lit/len list length is marked kInflateWide.  LIT = kLaneWideLit: the kInflateWide
+// members only.
+template <int LIT>
 __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
+    typedef LaneLayout<LIT> LL;
+    typedef typename LL::Cols Cols;
+    constexpr bool kWide = LIT != kLaneLitCap;
     extern __shared__ __attribute__((aligned(16))) uint16_t lcol[];
     PMC_LDS uint16_t *col = to_lds<uint16_t>(lcol + threadIdx.x);
-    PMC_LDS uint32_t *ring = to_lds<uint32_t>((uint8_t *)lcol + kLaneRingOff) + threadIdx.x;
-    PMC_LDS uint8_t *bcol = to_lds<uint8_t>((uint8_t *)lcol + kLaneRingOff + threadIdx.x);
-    PMC_LDS uint32_t *winw = to_lds<uint32_t>((uint8_t *)lcol + kLaneWinOff) + threadIdx.x;
+    PMC_LDS uint32_t *ring = to_lds<uint32_t>((uint8_t *)lcol + LL::kRingOff) + threadIdx.x;
+    PMC_LDS uint8_t *bcol = to_lds<uint8_t>((uint8_t *)lcol + LL::kRingOff + threadIdx.x);
+    PMC_LDS uint32_t *winw = to_lds<uint32_t>((uint8_t *)lcol + LL::kWinOff) + threadIdx.x;
     for (uint64_t vb = (uint64_t)blockIdx.x * 64; vb < a.n; vb += (uint64_t)gridDim.x * 64) {
         const uint64_t vi = vb + threadIdx.x;
         const uint64_t v = a.order && vi < a.n ? (uint64_t)a.order[vi] : vi;
         const uint32_t in_len = v < a.n ? a.src_len[v] : 0u;
-        // st: 0 decoding, 1 end of block reached, 2 declined, 3 no member / empty input
+        // st: 0 decoding, 1 end of block reached, 2 declined, 3 no member / empty input, 5 for the wide pass
         uint32_t st = v < a.n ? 0u : 3u;
-        if (st == 0 && a.big_only && a.rc[v] != kInflateBig) st = 3; // the record kernel's member
+        if (st == 0 && (kWide ? a.rc[v] != kInflateWide : a.big_only && a.rc[v] != kInflateBig))
+            st = 3; // not this pass's member (the record kernel's, or decoded by the first lane pass)
         if (st == 0 && in_len == 0) {
             a.rc[v] = PMC_INVALID_INPUT_DEV;
             a.dst_len[v] = 0;
@@ -499,15 +519,17 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
         in.len = st == 0 ? in_len : 0u;
         in.blk = (PMC_GLB const uint4 *)((uintptr_t)in.p & ~(uintptr_t)15);
         LaneCode<15> lit, dist;
-        lit.base = (PMC_LDS int16_t *)(col + kColBaseL * 64);
-        lit.sym = col + kColLit * 64;
-        dist.base = (PMC_LDS int16_t *)(col + kColBaseD * 64);
-        dist.sym = col + kColDist * 64;
+        lit.base = (PMC_LDS int16_t *)(col + Cols::kColBaseL * 64);
+        lit.sym = col + Cols::kColLit * 64;
+        dist.base = (PMC_LDS int16_t *)(col + Cols::kColBaseD * 64);
+        dist.sym = col + Cols::kColDist * 64;
         bool fixed = false;
 #ifdef PMC_STAMPS
         uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (st == 0 && !lane_prepare<LaneColsL>(in, col, bcol, lit, dist, fixed)) st = 2;
+        bool wide = false; // declined only for the lit/len list's length: the wide pass takes it
+        if (st == 0 && !lane_prepare<Cols>(in, col, bcol, lit, dist, fixed, &wide, kLaneWideLit, kLaneDistCap))
+            st = kWide || !wide ? 2u : 5u;
 #ifdef PMC_STAMPS
         uint64_t t1 = __builtin_amdgcn_s_memtime();
         uint64_t n_it = 0, n_act = 0;
@@ -632,6 +654,7 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
             }
         }
         if (st == 2) a.rc[v] = kInflateRetry;
+        if (st == 5) a.rc[v] = kInflateWide;
 #ifdef PMC_STAMPS
         // dbg slots 3..7 (the wave kernels' 0..5 see only retried members): wave iterations
         // of the decode loop, active lane-iterations, cycles in prepare, decode, finish
@@ -646,6 +669,9 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
 #endif
     }
 }
+
+template __global__ void inflate_lane_kernel<kLaneLitCap>(InflateArgs);
+template __global__ void inflate_lane_kernel<kLaneWideLit>(InflateArgs);
 
 // ---- visit order: counting sort of member indices by compressed length ------------------
 // Blocks take contiguous slices; bins are per-block LDS counts, one global add per used bin.

@@ -193,7 +193,8 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
         uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
         bool over = false;
-        if (st == 0 && !lane_prepare<RecCols>(in, col, bcol, lit, dist, fixed, &over)) st = over ? 4u : 2u;
+        if (st == 0 && !lane_prepare<RecCols>(in, col, bcol, lit, dist, fixed, &over, kLaneWideLit, kLaneDistCap))
+            st = over ? 4u : 2u; // (lists the lane kernels hold: theirs)
 #ifdef PMC_STAMPS
         uint64_t t1 = __builtin_amdgcn_s_memtime();
         uint64_t n_it = 0, n_act = 0;

@@ -111,6 +111,7 @@ __global__ void order_scatter_kernel(const uint32_t *src_len, uint64_t n, uint32
 
 constexpr int32_t kInflateRetry = -7777; // internal rc: lane fast path declined the member
 constexpr int32_t kInflateBig = -7779;   // internal rc: output beyond the record kernel's image
+constexpr int32_t kInflateWide = -7781;  // internal rc: lit/len code longer than the lane kernel's lists
 constexpr uint32_t kRecOutMax = 4096;    // record kernel: output image bytes per member
 constexpr uint32_t kRecMax = 2048;       // record kernel: records per member (scratch row)
 
@@ -129,6 +130,7 @@ __global__ void deflate_trees_kernel(DeflateArgs a);
 __global__ void deflate_back_kernel(DeflateArgs a);
 template <bool kHbm>
 __global__ void inflate_kernel(InflateArgs a);
+template <int LIT>
 __global__ void inflate_lane_kernel(InflateArgs a);
 __global__ void inflate_rec_kernel(InflateArgs a);
 __global__ void inflate_verify_kernel(InflateArgs a);

@@ -33,7 +33,10 @@ def main():
     corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).cuda()
     dbg = torch.zeros(32, dtype=torch.int64, device="cuda")
     L.pmc_debug_stamps(ctx.handle, dbg.data_ptr())
-    for vlen, kind, n in ((1024, 0, 400_000), (256, 0, 400_000), (4096, 0, 100_000), (1024, 1, 200_000)):
+    cases = ((1024, 0, 400_000), (256, 0, 400_000), (4096, 0, 100_000), (1024, 1, 200_000))
+    if len(sys.argv) > 1:  # e.g. 30000:0:20000
+        cases = tuple(tuple(int(x) for x in a.split(":")) for a in sys.argv[1:])
+    for vlen, kind, n in cases:
         data = torch.empty(n * vlen + 16, dtype=torch.uint8, device="cuda")
         L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), 0x5EED if kind == 0 else 0xA1B2, kind, 0, None, n,
                          vlen, data.data_ptr(), D.stream_handle())

@@ -135,3 +135,28 @@ def test_record_inflate_capacity_and_corrupt_verdicts(golden):
             assert dl[k] > caps[k], k
             assert O.decompress(v, cap=int(dl[k]), grow=False)[0] != O.CAPACITY, k
     assert short >= 7  # every "one short" member
+
+
+def test_large_members_decode_on_the_lane_passes(tmp_path):
+    """16-30 KB JSON members (the reference's own 5_*/6_* fixtures are 29-30 KB): a third of them use more
+    than 96 lit/len symbols, which the first lane pass declines and the wide pass (128-entry lists) takes.
+    Run in a child with PMC_DIAG_INFLATE_STOP=2 (verdicts after the CRC check, before the wave-kernel
+    retry): at least 99 % of the members must come back decoded, byte-exact, from the lane passes alone,
+    and the full path (retry included) must return every member."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    probe = os.path.join(root, "scripts", "inflate_probe.py")
+    out = {}
+    for stop in ("2", "0"):
+        r = subprocess.run([sys.executable, probe, "30000", "16000"], capture_output=True, text=True, timeout=600,
+                           env=dict(os.environ, PMC_DIAG_INFLATE_STOP=stop))
+        assert r.returncode == 0, r.stdout + r.stderr
+        for ln in r.stdout.splitlines():
+            if ln.startswith("stop="):
+                f = dict(x.split("=", 1) for x in ln.split()[:2])
+                out[(f["stop"], int(f["vlen"]))] = int(ln.rsplit(":", 1)[1])
+    for vlen in (30000, 16000):
+        assert out[("2", vlen)] >= 0.99 * 4096, out
+        assert out[("0", vlen)] == 4096, out
