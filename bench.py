@@ -116,7 +116,9 @@ def fullsize_parity(L, ctx, comp, coff, clen, n, vlen, kind, world, rank, sh):
     rec = torch.stack([clen, mcrc], dim=1).cpu().numpy().astype("<u4")
     got = hashlib.sha256(rec.tobytes()).hexdigest()
     return {"match": got == want["sha256"], "members": n, "sha256": got,
-            "method": "sha256 over the (u32 len, u32 CRC-32) record of every member, vs the reference's",
+            "method": "sha256 over the (u32 len, u32 CRC-32) record of every member, vs the reference's "
+                      "(a length + CRC-32 digest of the member bytes, not a byte-by-byte comparison; the "
+                      "byte-by-byte comparisons are the goldens, tests/test_gpu_codec.py)",
             "reference": f"tests/golden/{fname} (reference GzipCompressor::Compress, zlib "
                          f"{doc.get('zlib_version')})"}
 
@@ -503,8 +505,8 @@ def main():
             "data": "synthetic: JSON slices of the reference's tests/data corpus (SURVEY.md §8d generator, "
                     f"seed {seed:#x})" if args.kind == 0 else "synthetic: random [A-Za-z0-9]",
             "config": {"workload": f"{n} x {vlen} B values per GPU ({'JSON-slice' if args.kind == 0 else 'alnum'}), "
-                                   "batched gzip level-9 compress + decompress, device-resident, byte-checked "
-                                   "against the reference (fullsize_parity)",
+                                   "batched gzip level-9 compress + decompress, device-resident; every member "
+                                   "checked against the reference by a (length, CRC-32) digest (fullsize_parity)",
                        "values_per_gpu": n, "value_bytes": vlen, "total_values": n * world,
                        "partition": "MurmurHash3_x64_128('key'+i)[0] % 128 % n_gpus (NUM_SHARDS=128)",
                        "parallelism": f"shard-partitioned x{world}, no collective"},
