@@ -2,12 +2,12 @@
 # Builds the two libraries of a same-box A/B (scripts/ab_check.sh, gpu_abab.sh), in this container:
 #   A = pmc_codec/libpmc_codec.so      from the committed tree (git HEAD, or $BASE)
 #   B = pmc_codec/libpmc_codec_alt.so  from the working tree
-# Run `make -C poor-man-s-cache_amd` afterwards to put the working tree's build back as A.
+# (EXTRA_B="-DX=1" adds flags to B only.)  Run `make -C poor-man-s-cache_amd` afterwards to put the working tree's build back as A.
 set -e
 cd "$(dirname "$0")/.."
 BASE=${BASE:-HEAD}
 HIPFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -fvisibility=hidden"
-/opt/rocm/bin/hipcc $HIPFLAGS -Iinclude -o poor-man-s-cache_amd/pmc_codec/libpmc_codec_alt.so \
+/opt/rocm/bin/hipcc $HIPFLAGS ${EXTRA_B:-} -Iinclude -o poor-man-s-cache_amd/pmc_codec/libpmc_codec_alt.so \
     poor-man-s-cache_amd/csrc/pmc_codec.hip &
 T=$(mktemp -d)
 git archive "$BASE" poor-man-s-cache_amd/csrc include | tar -x -C "$T"
