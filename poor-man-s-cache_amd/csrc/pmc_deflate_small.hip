@@ -1876,9 +1876,10 @@ struct SmallWave {
     }
     // codes_from_lengths4 for the three trees at once (the split back's code-length row is
     // contiguous: lit/len 286 | dist 30 | bl 19; the code slots lcode 288 | dcode 32 | blcode 32 are
-    // too): a group is (tree, length), 6 ballots; counts at tmp[tree * 16 + L], next codes at
+    // too): a group is (tree, length); counts at tmp[tree * 16 + L], next codes at
     // tmp[48 + tree * 16 + L] from one in-row DPP scan whose rows are the trees (96 words of tmp).
-    // One call and one set of passes instead of three.
+    // One call and one set of passes instead of three.  (round 3: ranks from returning atomics
+    // instead of 6 ballots + a ds_bpermute per chunk)
     __device__ __noinline__ void codes_from_lengths_all(PMC_LDS const uint8_t *Ls, PMC_LDS uint32_t *code0,
                                                         PMC_LDS uint32_t *tmp) {
         constexpr int E = kLCodes + kDCodes + kBLCodes;
@@ -1890,18 +1891,10 @@ struct SmallWave {
             const int s = c0 + (int)l;
             const bool in = s < E;
             const uint32_t len = in ? Ls[s] : 0u, t = tree_of(s), key = t << 4 | len;
-            uint64_t m = ballot(in);
-#pragma unroll
-            for (int bt = 0; bt < 6; bt++) {
-                const uint64_t B = ballot((key >> bt) & 1);
-                m &= ((key >> bt) & 1) ? B : ~B;
-            }
-            const uint32_t rank = popc_lt(m);
-            uint32_t prior = 0;
-            if (in && len && rank == 0) prior = lds_add(&tmp[key], (uint32_t)__builtin_popcountll(m));
-            const uint32_t lead = m ? (uint32_t)__builtin_ctzll(m) : l;
-            prior = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead << 2), (int)prior);
-            if (in) code0[s + 2 * t] = prior + rank; // (slots: s, 288 + s - 286, 320 + s - 316)
+            // the symbol's rank among the earlier ones of its (tree, length): one returning LDS
+            // atomic (the lanes of one instruction get their old counts in lane order, and one
+            // wave's atomics apply in order across chunks; scripts/micro/lds_atomic_order.hip)
+            if (in) code0[s + 2 * t] = len ? lds_add(&tmp[key], 1u) : 0u; // (slots: s, 288 + s - 286, 320 + s - 316)
         }
         wave_sync();
         {
