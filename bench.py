@@ -360,6 +360,8 @@ def main():
     L = pmc_codec.lib()
     corpus_b = load_corpus()
     n, vlen = args.n, args.vlen
+    if args.kind == 0 and vlen > len(corpus_b):  # values longer than the 82 KB corpus: slices of it tiled
+        corpus_b = corpus_b * (vlen // len(corpus_b) + 2)
     seed = 0x5EED if args.kind == 0 else 0xA1B2
 
     # ---- CPU baseline first (host idle), rank 0 at N=1 only ------------------------------

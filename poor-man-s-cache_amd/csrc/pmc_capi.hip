@@ -470,8 +470,11 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     uint64_t hbm_waves = 0, hbm_wb = 0;
     if (max_len > hbm_cut || big_pass) {
         hbm_wb = deflate_wave_bytes(true, max_len);
-        hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 2,
-                                                             (8ull << 30) / std::max<uint64_t>(hbm_wb, 1)));
+        // as many waves as the kernel's 196 VGPRs let a CU hold (2 per SIMD) within a 32 GiB scratch
+        // budget: at 2 waves per CU (round 1-2) the latency-bound walk left 64 KiB values at
+        // 0.52 GiB/s
+        hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 8,
+                                                             (32ull << 30) / std::max<uint64_t>(hbm_wb, 1)));
         hbm_waves = std::min<uint64_t>(hbm_waves, n);
     }
     if (split) {
