@@ -38,6 +38,9 @@ def main():
         cases = tuple(tuple(int(x) for x in a.split(":")) for a in sys.argv[1:])
     for vlen, kind, n in cases:
         data = torch.empty(n * vlen + 16, dtype=torch.uint8, device="cuda")
+        if kind == 0 and vlen > len(corpus_b):  # (as bench.py: the corpus tiled for values longer than it)
+            corpus_b = corpus_b * (vlen // len(corpus_b) + 2)
+            corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).cuda()
         L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), 0x5EED if kind == 0 else 0xA1B2, kind, 0, None, n,
                          vlen, data.data_ptr(), D.stream_handle())
         off = torch.arange(n, dtype=torch.int64, device="cuda") * vlen
