@@ -719,11 +719,17 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
                     [&] { hipLaunchKernelGGL(inflate_rec_kernel, dim3(rb), dim3(64), kRecLdsBytes, st, a); });
             a.big_only = 1;
         }
+        // members of several blocks exist only above 16383 output bytes (zlib flushes every 16383
+        // symbols): then a third pass decodes them block after block
+        a.multi_pass = max_len > 16383 ? 1 : 0;
         klaunch(ctx, PMC_K_INFLATE_LANE, st, [&] {
-            hipLaunchKernelGGL(inflate_lane_kernel<kLaneLitCap>, dim3(lb), dim3(64), kLaneLdsBytes, st, a);
+            hipLaunchKernelGGL((inflate_lane_kernel<kLaneLitCap, false>), dim3(lb), dim3(64), kLaneLdsBytes, st, a);
             // members whose lit/len code did not fit its lists (a third of 30 KB JSON values): the wide
             // instance (it skips every other member at once)
-            hipLaunchKernelGGL(inflate_lane_kernel<kLaneWideLit>, dim3(lb), dim3(64), kLaneWideLdsBytes, st, a);
+            hipLaunchKernelGGL((inflate_lane_kernel<kLaneWideLit, false>), dim3(lb), dim3(64), kLaneWideLdsBytes, st, a);
+            if (a.multi_pass)
+                hipLaunchKernelGGL((inflate_lane_kernel<kLaneWideLit, true>), dim3(lb), dim3(64), kLaneMultiLdsBytes, st,
+                                   a);
         });
         a.big_only = 0;
         static const int diag_stop = getenv("PMC_DIAG_INFLATE_STOP") ? atoi(getenv("PMC_DIAG_INFLATE_STOP")) : 0;

@@ -60,15 +60,19 @@ constexpr uint32_t kWinDw = PMC_LANE_WIN, kWinHalf = kWinDw / 2;
 // kRing - 16 read dst (L2).  (128 fits five waves per CU but measured slower than 256 at four.)
 constexpr uint32_t kRing = PMC_LANE_RING, kFlush = kRing / 2;
 // the lane kernel's LDS per 64-lane block for lit/len lists of LIT entries: columns | rings | windows
-template <int LIT>
+// (MB, the multi-block pass: the build columns get their own region after the windows, because a
+// block's tables are built while the other lanes' rings hold live output)
+template <int LIT, bool MB = false>
 struct LaneLayout {
     typedef LaneCols<LIT, kLaneDistCap> Cols;
     static constexpr uint32_t kRingOff = (uint32_t)Cols::kColWords * 64 * 2; // output rings (LaneOut)
     static constexpr uint32_t kWinOff = kRingOff + kRing / 4 * 64 * 4;       // input windows (LaneWin)
-    static constexpr uint32_t kLds = kWinOff + kWinDw * 64 * 4;
+    static constexpr uint32_t kBColOff = kWinOff + kWinDw * 64 * 4;          // MB: build columns
+    static constexpr uint32_t kLds = kBColOff + (MB ? (kBColCl + 19) * 64 : 0);
 };
 constexpr uint32_t kLaneLdsBytes = LaneLayout<kLaneLitCap>::kLds;
 constexpr uint32_t kLaneWideLdsBytes = LaneLayout<kLaneWideLit>::kLds;
+constexpr uint32_t kLaneMultiLdsBytes = LaneLayout<kLaneWideLit, true>::kLds;
 static_assert((kBColCl + 19) * 64 <= kRing * 64, "build columns live in the output rings");
 
 // 16-byte load through a global (not flat) pointer: flat loads also count against lgkmcnt,
@@ -355,19 +359,12 @@ __device__ bool lane_lengths(LaneIn &in, const LaneClc &clc, uint32_t nlen, uint
     return true;
 }
 
-// Header and block header of a single-block fixed/dynamic member, code tables built;
-// false = decline (stored or multi-block members, header flags, malformed codes ...).  *over
-// (if given) is set when the only reason is C's list capacity: the lane kernel's lists hold it.
-// (wide_lit / wide_dist: the capacity *over tests against)
+// A block's header (after its BFINAL bit) and code tables, `in` at the BTYPE bits; false = decline.
 template <class C>
-__device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
-                             LaneCode<15> &dist, bool &fixed, bool *over = nullptr, int wide_lit = kLaneLitCap,
-                             int wide_dist = kLaneDistCap) {
-    if (in.len < 18) return false;
-    if (in.byte_at(0) != 0x1f || in.byte_at(1) != 0x8b || in.byte_at(2) != 8 || in.byte_at(3) != 0) return false;
-    in.seek(80);
-    const uint32_t bfinal = in.bits(1), btype = in.bits(2);
-    if (!bfinal || btype == 0 || btype == 3) return false;
+__device__ bool lane_block(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
+                           LaneCode<15> &dist, bool &fixed, bool *over, int wide_lit, int wide_dist) {
+    const uint32_t btype = in.bits(2);
+    if (btype == 0 || btype == 3) return false;
     fixed = btype == 1;
     if (fixed) return true;
     const uint32_t nlit = in.bits(5) + 257, ndist = in.bits(5) + 1, ncl = in.bits(4) + 4;
@@ -435,6 +432,27 @@ __device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t 
     return true;
 }
 
+// Header and block header of a single-block fixed/dynamic member, code tables built;
+// false = decline (stored or multi-block members, header flags, malformed codes ...).  *over
+// (if given) is set when the only reason is C's list capacity: the lane kernel's lists hold it;
+// *multi (if given) when the member's first block is not its last (the multi-block pass takes it).
+// (wide_lit / wide_dist: the capacity *over tests against)
+template <class C>
+__device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
+                             LaneCode<15> &dist, bool &fixed, bool *over = nullptr, int wide_lit = kLaneLitCap,
+                             int wide_dist = kLaneDistCap, bool *multi = nullptr, uint32_t *last = nullptr) {
+    if (in.len < 18) return false;
+    if (in.byte_at(0) != 0x1f || in.byte_at(1) != 0x8b || in.byte_at(2) != 8 || in.byte_at(3) != 0) return false;
+    in.seek(80);
+    const uint32_t bfinal = in.bits(1);
+    if (last) *last = bfinal;
+    if (!bfinal && !last) {
+        if (multi) *multi = true;
+        return false;
+    }
+    return lane_block<C>(in, col, bcol, lit, dist, fixed, over, wide_lit, wide_dist);
+}
+
 // Output of one lane: the last kRing bytes live in an LDS ring (column layout, dword k of
 // the ring at word k * 64 of the lane's column) aligned so that ring dwords map onto dst
 // dwords; complete dwords go to dst in bursts of >= kFlush bytes.  Keeping the byte-level
@@ -488,17 +506,19 @@ struct LaneOut {
 };
 
 // LIT = kLaneLitCap: every member (a.big_only: those the record kernel marked kInflateBig); a member
-// declined only for its lit/len list length is marked kInflateWide.  LIT = kLaneWideLit: the kInflateWide
-// members only.
-template <int LIT>
+// declined only for its lit/len list length is marked kInflateWide, one of several blocks kInflateMulti
+// (when a.multi_pass).  LIT = kLaneWideLit: the kInflateWide members only.  MB: the kInflateMulti members,
+// block after block (a block boundary re-reads the header and rebuilds the tables from the decode
+// window's bit position; values above 16383 bytes, whose members zlib splits every 16383 symbols).
+template <int LIT, bool MB>
 __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
-    typedef LaneLayout<LIT> LL;
+    typedef LaneLayout<LIT, MB> LL;
     typedef typename LL::Cols Cols;
-    constexpr bool kWide = LIT != kLaneLitCap;
+    constexpr bool kWide = LIT != kLaneLitCap && !MB;
     extern __shared__ __attribute__((aligned(16))) uint16_t lcol[];
     PMC_LDS uint16_t *col = to_lds<uint16_t>(lcol + threadIdx.x);
     PMC_LDS uint32_t *ring = to_lds<uint32_t>((uint8_t *)lcol + LL::kRingOff) + threadIdx.x;
-    PMC_LDS uint8_t *bcol = to_lds<uint8_t>((uint8_t *)lcol + LL::kRingOff + threadIdx.x);
+    PMC_LDS uint8_t *bcol = to_lds<uint8_t>((uint8_t *)lcol + (MB ? LL::kBColOff : LL::kRingOff) + threadIdx.x);
     PMC_LDS uint32_t *winw = to_lds<uint32_t>((uint8_t *)lcol + LL::kWinOff) + threadIdx.x;
     for (uint64_t vb = (uint64_t)blockIdx.x * 64; vb < a.n; vb += (uint64_t)gridDim.x * 64) {
         const uint64_t vi = vb + threadIdx.x;
@@ -506,7 +526,8 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
         const uint32_t in_len = v < a.n ? a.src_len[v] : 0u;
         // st: 0 decoding, 1 end of block reached, 2 declined, 3 no member / empty input, 5 for the wide pass
         uint32_t st = v < a.n ? 0u : 3u;
-        if (st == 0 && (kWide ? a.rc[v] != kInflateWide : a.big_only && a.rc[v] != kInflateBig))
+        if (st == 0 && (MB ? a.rc[v] != kInflateMulti
+                           : kWide ? a.rc[v] != kInflateWide : a.big_only && a.rc[v] != kInflateBig))
             st = 3; // not this pass's member (the record kernel's, or decoded by the first lane pass)
         if (st == 0 && in_len == 0) {
             a.rc[v] = PMC_INVALID_INPUT_DEV;
@@ -527,9 +548,12 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
 #ifdef PMC_STAMPS
         uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-        bool wide = false; // declined only for the lit/len list's length: the wide pass takes it
-        if (st == 0 && !lane_prepare<Cols>(in, col, bcol, lit, dist, fixed, &wide, kLaneWideLit, kLaneDistCap))
-            st = kWide || !wide ? 2u : 5u;
+        bool wide = false;  // declined only for the lit/len list's length: the wide pass takes it
+        bool multi = false; // declined only for having several blocks: the multi-block pass takes it
+        uint32_t blast = 1; // MB: the current block is the member's last
+        if (st == 0 && !lane_prepare<Cols>(in, col, bcol, lit, dist, fixed, &wide, kLaneWideLit, kLaneDistCap, &multi,
+                                           MB ? &blast : nullptr))
+            st = multi && a.multi_pass ? 7u : kWide || MB || !wide ? 2u : 5u;
 #ifdef PMC_STAMPS
         uint64_t t1 = __builtin_amdgcn_s_memtime();
         uint64_t n_it = 0, n_act = 0;
@@ -581,7 +605,7 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
                             }
                         }
                     } else if (sy == 256) {
-                        st = 1;
+                        st = MB && !blast ? 6u : 1u;
                     } else if (sy > 285) {
                         st = 2;
                     } else {
@@ -623,6 +647,17 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
                     o.pos += m;
                     rem -= m;
                 }
+                if (MB && st == 6) { // end of a block that is not the last: the next one's header and tables
+                    in.seek(win.bitpos());
+                    blast = in.bits(1);
+                    bool ov = false;
+                    if (lane_block<Cols>(in, col, bcol, lit, dist, fixed, &ov, kLaneWideLit, kLaneDistCap)) {
+                        win.start(in, in.bitpos());
+                        st = 0;
+                    } else {
+                        st = 2; // stored blocks, longer lists, malformed codes: the wave kernel
+                    }
+                }
             }
             // wave-synchronous flush: every lane writes its complete dwords at once, so the
             // wave waits for stores a few times per member instead of once per lane flush
@@ -655,6 +690,7 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
         }
         if (st == 2) a.rc[v] = kInflateRetry;
         if (st == 5) a.rc[v] = kInflateWide;
+        if (st == 7) a.rc[v] = kInflateMulti;
 #ifdef PMC_STAMPS
         // dbg slots 3..7 (the wave kernels' 0..5 see only retried members): wave iterations
         // of the decode loop, active lane-iterations, cycles in prepare, decode, finish
@@ -670,8 +706,9 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
     }
 }
 
-template __global__ void inflate_lane_kernel<kLaneLitCap>(InflateArgs);
-template __global__ void inflate_lane_kernel<kLaneWideLit>(InflateArgs);
+template __global__ void inflate_lane_kernel<kLaneLitCap, false>(InflateArgs);
+template __global__ void inflate_lane_kernel<kLaneWideLit, false>(InflateArgs);
+template __global__ void inflate_lane_kernel<kLaneWideLit, true>(InflateArgs);
 
 // ---- visit order: counting sort of member indices by compressed length ------------------
 // Blocks take contiguous slices; bins are per-block LDS counts, one global add per used bin.

@@ -100,6 +100,7 @@ struct InflateArgs {
     int32_t stop_after;    // PMC_STAMPS / PMC_PHASE_STOP builds: record kernel ends after phase k
     uint32_t *rec_work;    // record kernel: work counter (64-member batches handed out), zeroed per launch
     uint32_t rec_max_out;  // record kernel: members of more output go to the lane kernel (<= kRecOutMax)
+    int32_t multi_pass;    // lane kernel: the multi-block pass runs (mark such members kInflateMulti)
 };
 
 // lane-inflate visit order: member indices grouped by compressed length, so a wave's 64
@@ -112,6 +113,7 @@ __global__ void order_scatter_kernel(const uint32_t *src_len, uint64_t n, uint32
 constexpr int32_t kInflateRetry = -7777; // internal rc: lane fast path declined the member
 constexpr int32_t kInflateBig = -7779;   // internal rc: output beyond the record kernel's image
 constexpr int32_t kInflateWide = -7781;  // internal rc: lit/len code longer than the lane kernel's lists
+constexpr int32_t kInflateMulti = -7783; // internal rc: a member of several blocks (the multi-block lane pass)
 constexpr uint32_t kRecOutMax = 4096;    // record kernel: output image bytes per member
 constexpr uint32_t kRecMax = 2048;       // record kernel: records per member (scratch row)
 
@@ -130,7 +132,7 @@ __global__ void deflate_trees_kernel(DeflateArgs a);
 __global__ void deflate_back_kernel(DeflateArgs a);
 template <bool kHbm>
 __global__ void inflate_kernel(InflateArgs a);
-template <int LIT>
+template <int LIT, bool MB>
 __global__ void inflate_lane_kernel(InflateArgs a);
 __global__ void inflate_rec_kernel(InflateArgs a);
 __global__ void inflate_verify_kernel(InflateArgs a);

@@ -1,5 +1,6 @@
 """Diagnostic: which members each inflate stage accepts (PMC_DIAG_INFLATE_STOP=1: after the record / lane
-kernels, 2: after the CRC check), by value size.  usage: python scripts/inflate_probe.py 30000 16000 4096"""
+kernels, 2: after the CRC check), by value size.  usage: python scripts/inflate_probe.py 30000 16000 4096 300000:32
+(vlen[:n], n = 4096 by default; values longer than the corpus are slices of it tiled)"""
 import os
 import subprocess
 import sys
@@ -24,8 +25,11 @@ ctx = pmc_codec.Context(0)
 d = os.path.join(ROOT, "tests", "golden", "data")
 cb = b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)) if f.endswith(".json"))
 corpus = torch.frombuffer(bytearray(cb), dtype=torch.uint8).cuda()
-for vlen in [int(x) for x in sys.argv[1:]] or [30000]:
-    n = 4096
+for arg in sys.argv[1:] or ["30000"]:
+    vlen, n = (int(x) for x in arg.split(":")) if ":" in arg else (int(arg), 4096)
+    if vlen > len(cb):
+        cb = cb * (vlen // len(cb) + 2)
+        corpus = torch.frombuffer(bytearray(cb), dtype=torch.uint8).cuda()
     data = torch.empty(n * vlen + 16, dtype=torch.uint8, device="cuda")
     assert L.pmc_gen_values(corpus.data_ptr(), len(cb), 0x5EED, 0, 0, None, n, vlen, data.data_ptr(),
                             D.stream_handle()) == 0

@@ -160,3 +160,26 @@ def test_large_members_decode_on_the_lane_passes(tmp_path):
     for vlen in (30000, 16000):
         assert out[("2", vlen)] >= 0.99 * 4096, out
         assert out[("0", vlen)] == 4096, out
+
+
+@pytest.mark.gpu
+def test_multiblock_members_decode_in_the_lane_pass():
+    """Members of several DEFLATE blocks (zlib flushes every 16383 symbols: 100 KB and 300 KB JSON values)
+    decode in the multi-block lane pass, block after block, not in the wave-per-member retry kernel:
+    with PMC_DIAG_INFLATE_STOP=2 (verdicts before the retry) every member comes back byte-exact."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    probe = os.path.join(root, "scripts", "inflate_probe.py")
+    out = {}
+    for stop in ("2", "0"):
+        r = subprocess.run([sys.executable, probe, "100000:128", "300000:24"], capture_output=True, text=True,
+                           timeout=600, env=dict(os.environ, PMC_DIAG_INFLATE_STOP=stop))
+        assert r.returncode == 0, r.stdout + r.stderr
+        for ln in r.stdout.splitlines():
+            if ln.startswith("stop="):
+                f = dict(x.split("=", 1) for x in ln.split()[:2])
+                out[(f["stop"], int(f["vlen"]))] = int(ln.rsplit(":", 1)[1])
+    for vlen, n in ((100000, 128), (300000, 24)):
+        assert out[("2", vlen)] == n and out[("0", vlen)] == n, out
