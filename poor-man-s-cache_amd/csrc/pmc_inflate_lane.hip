@@ -361,7 +361,7 @@ __device__ bool lane_lengths(LaneIn &in, const LaneClc &clc, uint32_t nlen, uint
 
 // A block's header (after its BFINAL bit) and code tables, `in` at the BTYPE bits; false = decline.
 template <class C>
-__device__ bool lane_block(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
+__device__ __forceinline__ bool lane_block(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
                            LaneCode<15> &dist, bool &fixed, bool *over, int wide_lit, int wide_dist) {
     const uint32_t btype = in.bits(2);
     if (btype == 0 || btype == 3) return false;
@@ -438,7 +438,7 @@ __device__ bool lane_block(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *b
 // *multi (if given) when the member's first block is not its last (the multi-block pass takes it).
 // (wide_lit / wide_dist: the capacity *over tests against)
 template <class C>
-__device__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
+__device__ __forceinline__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
                              LaneCode<15> &dist, bool &fixed, bool *over = nullptr, int wide_lit = kLaneLitCap,
                              int wide_dist = kLaneDistCap, bool *multi = nullptr, uint32_t *last = nullptr) {
     if (in.len < 18) return false;
