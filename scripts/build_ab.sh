@@ -15,4 +15,6 @@ git archive "$BASE" poor-man-s-cache_amd/csrc include | tar -x -C "$T"
     "$T/poor-man-s-cache_amd/csrc/pmc_codec.hip"
 wait
 rm -rf "$T"
+# A is a HEAD build with a fresh mtime: make the working-tree sources newer so the next `make` rebuilds it
+touch poor-man-s-cache_amd/csrc/pmc_codec.hip
 echo "A = $BASE, B = working tree"
