@@ -758,8 +758,8 @@ __global__ void __launch_bounds__(256) order_scatter_kernel(const uint32_t *src_
 // CRC-32 of the members g + j (j in `todo`) of a batch of byte strings, returned in lane j.
 // Members of up to kCrcQuarterMax bytes go four to a wave: quarter q (16 lanes) takes the
 // q-th member of the round, lane s of it the s-th 64-byte piece counted from the member's
-// END, front-padded with zero bytes.  A piece runs slicing-by-8 from register 0 (17 dword
-// loads, v_alignbyte for the member's byte alignment); the quarter then folds its pieces in
+// END, front-padded with zero bytes.  A piece runs slicing-by-8 from register 0 (17 dwords from
+// five 16-byte loads, v_alignbyte for the member's byte alignment); the quarter then folds its pieces in
 // four DPP row_shl levels, shifting the earlier half past 64*2^k bytes with a 4x256 table,
 // and the init value's share 0xFFFFFFFF x^(8 len) comes from c_crc_ones (zeros in front of
 // a register-0 CRC leave it unchanged, so the padding is free).  Longer members take the
@@ -768,18 +768,31 @@ __device__ __forceinline__ uint32_t crc_piece64(const uint8_t *buf, uint64_t off
                                                 PMC_LDS const uint32_t *s8) {
     const int64_t pend = (int64_t)len - (int64_t)kCrcPiece * s, pbeg = pend - kCrcPiece;
     const uint64_t base = (uint64_t)buf + off;
-    const uint64_t lo = base & ~(uint64_t)3, hi = (base + len - 1) & ~(uint64_t)3;
     const uint64_t ab = (uint64_t)((int64_t)base + pbeg) & ~(uint64_t)3;
     const uint32_t sh = (uint32_t)(base + (uint64_t)pend) & 3;
     const int32_t lead = pbeg < 0 ? (int32_t)-pbeg : 0;
+    // the piece's 17 dwords from five 16-byte loads (one pass of the address unit per 16 bytes, not
+    // per dword: with 64 lanes on 32 lines per instruction, 17 dword loads had made this kernel
+    // L1-bound), each block clamped to the member's first / last 16-byte block (a block that holds
+    // none of the member's bytes only feeds bytes the lead mask or the alignment drop)
+    const uint64_t a16 = ab & ~(uint64_t)15, lo16 = base & ~(uint64_t)15, hi16 = (base + len - 1) & ~(uint64_t)15;
+    const uint32_t o = (uint32_t)(ab - a16) >> 2;
+    uint32_t d[20];
+#pragma unroll
+    for (int b = 0; b < 5; b++) {
+        uint64_t p = a16 + 16 * b;
+        p = p < lo16 ? lo16 : p;
+        p = p > hi16 ? hi16 : p;
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u v = *(const PMC_GLB v4u *)p;
+        d[4 * b] = v.x;
+        d[4 * b + 1] = v.y;
+        d[4 * b + 2] = v.z;
+        d[4 * b + 3] = v.w;
+    }
     uint32_t w[17];
 #pragma unroll
-    for (int i = 0; i < 17; i++) {
-        uint64_t p = ab + 4 * i;
-        p = p < lo ? lo : p;
-        p = p > hi ? hi : p;
-        w[i] = *(const PMC_GLB uint32_t *)p;
-    }
+    for (int i = 0; i < 17; i++) w[i] = o == 0 ? d[i] : o == 1 ? d[i + 1] : o == 2 ? d[i + 2] : d[i + 3];
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
