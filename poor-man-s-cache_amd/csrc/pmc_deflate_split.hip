@@ -293,9 +293,29 @@ struct LaneTrees {
         return max_code;
     }
 
-    // scan_tree (trees.c): bit-length tree frequencies for lengths lens[row0 .. row0 + max_code]
+    // byte j of the lengths row as staged in the heap column (stage_row)
+    __device__ uint32_t lrow(uint32_t j) const { return (hp[(j >> 2) * 64] >> (8 * (j & 3))) & 0xffu; }
+    // The lit/len + distance lengths (row bytes 0..319) into the heap column, free between the distance
+    // tree's build and the bit-length tree's: twenty 16-byte loads in flight at once, so scan_tree reads
+    // LDS.  (Reading the row from HBM eight bytes per step made it ~40 dependent global round trips per
+    // value, most of one value's trees latency: 243 us for a lone 1 KiB value.)
+    __device__ void stage_row() {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        v4u r[20];
+#pragma unroll
+        for (int i = 0; i < 20; i++) r[i] = *(PMC_GLB const v4u *)(lens + 16 * i);
+#pragma unroll
+        for (int i = 0; i < 20; i++) {
+            hp[(4 * i + 0) * 64] = r[i].x;
+            hp[(4 * i + 1) * 64] = r[i].y;
+            hp[(4 * i + 2) * 64] = r[i].z;
+            hp[(4 * i + 3) * 64] = r[i].w;
+        }
+    }
+
+    // scan_tree (trees.c): bit-length tree frequencies for lengths row[row0 .. row0 + max_code] (staged)
     __device__ void scan(uint32_t row0, int max_code) {
-        int prevlen = -1, nextlen = lens[row0], count = 0, max_count = 7, min_count = 4;
+        int prevlen = -1, nextlen = (int)lrow(row0), count = 0, max_count = 7, min_count = 4;
         if (nextlen == 0) max_count = 138, min_count = 3;
         int w0 = -8;
         uint64_t pk = 0; // lengths w0 .. w0 + 7, one byte each (fetched 8 at a time so the loads overlap)
@@ -307,7 +327,7 @@ struct LaneTrees {
                     pk = 0;
 #pragma unroll
                     for (int k = 0; k < 8; k++)
-                        pk |= (uint64_t)(w0 + k <= max_code ? lens[row0 + w0 + k] : 0u) << (8 * k);
+                        pk |= (uint64_t)(w0 + k <= max_code ? lrow(row0 + (uint32_t)(w0 + k)) : 0u) << (8 * k);
                 }
                 nextlen = (int)((pk >> (8 * (nx - w0))) & 0xff);
             } else {
@@ -357,13 +377,23 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC
     auto dhist = [&](int s) -> uint32_t { return t.hist[kLCodes + s]; };
     const int d_max = t.build(dhist, kDCodes, kLCodes, 1, kMaxBits, opt, stat);
     for (int s = 0; s < kBLCodes; s++) t.blf[s * 64] = 0;
+    t.stage_row();
     t.scan(0, l_max);
     t.scan(kLCodes, d_max);
     auto bfreq = [&](int s) -> uint32_t { return t.blf[s * 64]; };
     t.build(bfreq, kBLCodes, kLCodes + kDCodes, 2, kMaxBLBits, opt, stat);
-    int mbi;
-    for (mbi = kBLCodes - 1; mbi >= 3; mbi--)
-        if (t.lens[kLCodes + kDCodes + bl_order_cf(mbi)] != 0) break;
+    // max_blindex from the bit-length code's lengths (row bytes 316..334) loaded at once, not one
+    // dependent HBM read per step of the loop
+    static_assert(kLCodes + kDCodes == 316 && kSplitRows >= 336, "bl lengths at row bytes 316..334");
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u q0 = *(PMC_GLB const v4u *)(t.lens + 304), q1 = *(PMC_GLB const v4u *)(t.lens + 320);
+    const uint32_t blw[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    int mbi = 2;
+#pragma unroll
+    for (int k = kBLCodes - 1; k >= 3; k--) {
+        const int j = 12 + (int)bl_order_cf(k); // byte of row 316 + bl_order(k), counted from 304
+        if (mbi == 2 && ((blw[j >> 2] >> (8 * (j & 3))) & 0xffu) != 0) mbi = k;
+    }
     opt += 3 * ((uint32_t)mbi + 1) + 5 + 5 + 4;
     uint32_t opt_lenb = (opt + 3 + 7) >> 3;
     const uint32_t static_lenb = (stat + 3 + 7) >> 3;
