@@ -374,7 +374,20 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC
         a.cD[atomicAdd(a.cD + a.count, 1u)] = (uint32_t)v;
         return;
     }
-    auto dhist = [&](int s) -> uint32_t { return t.hist[kLCodes + s]; };
+    // the distance frequencies (row u16 286..315, bytes 572..631) staged in heap slots 60..74 with five
+    // 16-byte loads at once; the distance tree's leaves fill slots 1..30 only (not four dependent HBM reads)
+    {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        PMC_GLB const v4u *g4 = (PMC_GLB const v4u *)t.hist;
+        static_assert(kLCodes * 2 == 35 * 16 + 12 && kDCodes == 30, "distance row at v4u 35, byte 12");
+        static_assert(CAP >= 75, "heap slots 60..74 hold the staged distance frequencies");
+        v4u d5[5];
+#pragma unroll
+        for (int i = 0; i < 5; i++) d5[i] = g4[35 + i];
+#pragma unroll
+        for (int j = 3; j < 18; j++) t.hp[(57 + j) * 64] = d5[j >> 2][j & 3];
+    }
+    auto dhist = [&](int s) -> uint32_t { return (t.hp[(60 + (s >> 1)) * 64] >> (16 * (s & 1))) & 0xffffu; };
     const int d_max = t.build(dhist, kDCodes, kLCodes, 1, kMaxBits, opt, stat);
     for (int s = 0; s < kBLCodes; s++) t.blf[s * 64] = 0;
     t.stage_row();
