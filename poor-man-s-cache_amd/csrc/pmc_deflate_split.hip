@@ -220,10 +220,10 @@ struct LaneTrees {
         uint32_t overflow = 0;
         for (int b = 0; b <= kMaxBits; b++) blc[b * 64] = 0;
         setH(K, 0);
-        // The merge list is read back 8 merges (16 keys) per batch with the next batch in flight:
+        // The merge list is read back 8 merges (16 keys) per batch with the next two batches in flight:
         // one dependent global round trip per merge made this replay the kernel's longest wait.
         constexpr int kB = 8;
-        uint32_t cur[2 * kB], nxt[2 * kB];
+        uint32_t cur[2 * kB], nxt[2 * kB], nx2[2 * kB];
         auto fetch = [&](int hi, uint32_t *d) { // merges hi - 1, hi - 2, ..., hi - kB (those >= 0)
 #pragma unroll
             for (int t = 0; t < kB; t++) {
@@ -232,9 +232,11 @@ struct LaneTrees {
                 d[2 * t + 1] = j >= 0 ? mg[(2 * j) * 64] : 0u;
             }
         };
+        // (two batches in flight ahead of the one being replayed)
         fetch((int)K, cur);
+        fetch((int)K - kB, nxt);
         for (int i0 = (int)K; i0 >= 1; i0 -= kB) {
-            fetch(i0 - kB, nxt);
+            fetch(i0 - 2 * kB, nx2);
 #pragma unroll
             for (int t = 0; t < kB; t++) {
                 const int i = i0 - t;
@@ -261,7 +263,10 @@ struct LaneTrees {
                 }
             }
 #pragma unroll
-            for (int t = 0; t < 2 * kB; t++) cur[t] = nxt[t];
+            for (int t = 0; t < 2 * kB; t++) {
+                cur[t] = nxt[t];
+                nxt[t] = nx2[t];
+            }
         }
         if (overflow) {
             int ov = (int)overflow;
