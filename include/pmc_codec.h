@@ -285,6 +285,16 @@ int pmc_debug_stamps(pmc_ctx *ctx, uint64_t *dev_buf);
 int pmc_ctx_profile(pmc_ctx *ctx, int enable);
 int pmc_ctx_kernel_times(pmc_ctx *ctx, double *ms, uint32_t *launches, int nkinds);
 
+/* Lane-order guards (build-owned; no reference counterpart).  The throughput compressor's hash
+ * sort and canonical-code ranks take a lane's rank from a returning LDS atomic, relying on the
+ * lanes of one ds_add_rtn_u32 that hit the same word getting their old values in lane order
+ * (measured on gfx950, not documented).  Every value is checked where the data already is; a value
+ * that fails is recompressed by the HBM kernel, which does not rely on it, so output stays
+ * bit-exact.  Synchronizes the device and copies out the context's counters: counts[0] values
+ * whose sort failed the check, counts[1] values whose code ranks failed it, counts[2] violations
+ * in pmc_ctx_create's self-test (nonzero: the context compresses through the single-kernel path). */
+int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[3]);
+
 #ifdef __cplusplus
 }
 #endif

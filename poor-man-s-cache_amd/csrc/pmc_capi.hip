@@ -171,6 +171,10 @@ struct pmc_ctx {
     DevBuf crcx;                 // inflate: CRC-32 trailers from the lane kernel
     DevBuf order;                // inflate: lane visit order (bins | member indices)
     DevBuf recs;                 // inflate: the record kernel's per-lane record rows
+    // lane-order guards (DeflateArgs::guard): u32 [0] sort, [1] code ranks, [2] the create-time probe's
+    // violations; lane_order_ok = the probe passed (else compress takes the kernels that do not need it)
+    DevBuf guard;
+    bool lane_order_ok = true;
     // per direction (0 compress, 1 decompress): the event recorded after the last batch call and its
     // stream; a call on another stream waits for it, since both use the direction's scratch
     hipEvent_t dir_ev[2] = {};
@@ -365,7 +369,29 @@ PMC_API int pmc_ctx_create(int device, pmc_ctx **out) {
         delete c;
         return PMC_E_NO_DEVICE;
     }
+    // guard counters, and the lane-order self-test (lane_order_probe_kernel: 4 waves x 512 trials)
+    uint32_t probe = 0;
+    if (c->guard.ensure(16) || hipMemsetAsync(c->guard.p, 0, 16, c->stream) != hipSuccess) {
+        pmc_ctx_destroy(c);
+        return PMC_E_NO_DEVICE;
+    }
+    hipLaunchKernelGGL(lane_order_probe_kernel, dim3(1), dim3(256), 0, c->stream, 512u, (uint32_t *)c->guard.p + 2);
+    if (hipMemcpyAsync(&probe, (uint32_t *)c->guard.p + 2, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        set_err("lane_order_probe_kernel", hipGetLastError());
+        pmc_ctx_destroy(c);
+        return PMC_E_NO_DEVICE;
+    }
+    c->lane_order_ok = probe == 0;
     *out = c;
+    return PMC_OK;
+}
+
+PMC_API int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[3]) {
+    if (!ctx || !counts) return PMC_E_ARG;
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(counts, ctx->guard.p, 12, hipMemcpyDeviceToHost));
     return PMC_OK;
 }
 
@@ -379,6 +405,7 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     c->split.release();
     c->crcx.release();
     c->recs.release();
+    c->guard.release();
     for (auto &r : c->krecs) {
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
@@ -444,7 +471,10 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
                            dim3(256), 0, st, src_len, (uint64_t)n, (uint64_t)max_len, rc, dst_len);
     DeflateArgs a{src, src_off, src_len, dst, dst_off, dst_cap, dst_len, rc, n, 0, 0, 0, nullptr, nullptr,
                   ctx->dbg, -1};
+    a.guard = (uint32_t *)ctx->guard.p;
+#if defined(PMC_STAMPS) || defined(PMC_PHASE_STOP)
     if (const char *e = getenv("PMC_STOP_AFTER")) a.stop_after = atoi(e); // diagnostic builds only
+#endif
     // Values <= small_lim (16382): the split pipeline's small pass; 16382 < len <= big_lim (~31.9K,
     // the front's 160 KiB LDS; MAX_DIST caps it at 32506): its large pass; the rest -- and
     // large-pass values of >= 16383 symbols, which need several DEFLATE blocks -- the general
@@ -452,7 +482,9 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     // through the general kernels (A/B and safety net); PMC_DEFLATE_MONO=1 the single-kernel path.
     static const bool force_v1 = getenv("PMC_DEFLATE_V1") && atoi(getenv("PMC_DEFLATE_V1"));
     static const bool mono_env = getenv("PMC_DEFLATE_MONO") && atoi(getenv("PMC_DEFLATE_MONO"));
-    const bool mono = mono_env || latency;
+    // (a context whose lane-order probe failed compresses through the single-kernel path, whose
+    // sort and codes use per-lane counters and ballots instead of returning-atomic ranks)
+    const bool mono = mono_env || latency || !ctx->lane_order_ok;
     static const bool no_big = getenv("PMC_BIG_PASS") && !atoi(getenv("PMC_BIG_PASS"));
     const bool split = !force_v1 && !mono;
     const uint64_t small_lim = force_v1 ? 0 : deflate_small_limit();
@@ -467,16 +499,21 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     const uint64_t big_hi = big_pass ? std::min<uint64_t>(big_lim, max_len) : 0;
     const uint64_t big_cap = big_pass ? std::min<uint64_t>((big_hi + 63) & ~(uint64_t)63, big_lim) : 0;
     const uint64_t hbm_cut = big_pass ? big_hi : lds_cut; // the HBM kernel takes lengths above this
-    uint64_t hbm_waves = 0, hbm_wb = 0;
-    if (max_len > hbm_cut || big_pass) {
-        hbm_wb = deflate_wave_bytes(true, max_len);
+    uint64_t hbm_waves = 0, hbm_wb = deflate_wave_bytes(true, max_len);
+    // without values for the HBM kernel it still runs, gated, as the lane-order guards' retry pass:
+    // it returns at once while no guard has fired in this context
+    const bool gated = !(max_len > hbm_cut || big_pass);
+    if (!gated) {
         // as many waves as the kernel's 196 VGPRs let a CU hold (2 per SIMD) within a 32 GiB scratch
         // budget: at 2 waves per CU (round 1-2) the latency-bound walk left 64 KiB values at
         // 0.52 GiB/s
         hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 8,
                                                              (32ull << 30) / std::max<uint64_t>(hbm_wb, 1)));
-        hbm_waves = std::min<uint64_t>(hbm_waves, n);
+    } else {
+        // (the single-kernel path's sort and codes do not use returning-atomic ranks: no retry pass)
+        hbm_waves = split ? (uint64_t)ctx->cus : 0;
     }
+    hbm_waves = std::min<uint64_t>(hbm_waves, n);
     if (split) {
         // chunk scratch budget (PMC_SPLIT_CHUNK_MB): 96 GiB of the 288 GiB holds 14M 1-KiB values, so the
         // 10M north-star batch is one front/trees/back launch set (~7 KB of chunk arrays per 1 KiB value,
@@ -629,7 +666,8 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     if (hbm_waves) {
         a.cap_len = max_len;
         a.lds_max_len = hbm_cut;
-        a.retry = big_pass ? 1 : 0;
+        a.retry = 1; // (large-pass values of several blocks, and values a lane-order guard declined)
+        a.gate = gated ? 1 : 0;
         a.wave_bytes = hbm_wb;
         a.scratch = (uint8_t *)ctx->dscratch.p;
         klaunch(ctx, PMC_K_DEFLATE_HBM, st, [&] {
@@ -904,7 +942,12 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
         const void *old = ctx->zc.p;
         r = ctx->zc.ensure(down + up);
         if (r) return r;
-        if (ctx->zc.p != old) HIP_TRY(hipHostGetDevicePointer(&ctx->zc_dev, ctx->zc.p, 0));
+        if (ctx->zc.p != old) ctx->zc_dev = nullptr; // (a new buffer: its device address is looked up below)
+        if (!ctx->zc_dev) {
+            void *d = nullptr;
+            HIP_TRY(hipHostGetDevicePointer(&d, ctx->zc.p, 0));
+            ctx->zc_dev = d;
+        }
         hp = (uint8_t *)ctx->zc.p;
         dp = (uint8_t *)ctx->zc_dev;
     } else {
@@ -960,7 +1003,12 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
             if (!r) r = r2;
         }
     }
-    if (r) return r;
+    if (r) {
+        // kernels already queued may still read or write the staging (in zero-copy mode the host
+        // buffers themselves), which the next call refills: let them drain before returning
+        (void)hipStreamSynchronize(st);
+        return r;
+    }
     if (!zc) HIP_TRY(hipMemcpyAsync(h_dlen, d_dlen, up, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     uint64_t po = 0;

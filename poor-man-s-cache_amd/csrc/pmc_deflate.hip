@@ -507,6 +507,9 @@ struct DeflateWave {
 // kHbm=true : working set in scratch + wave * wave_bytes (HBM); CRC table still in LDS.
 template <bool kHbm>
 __global__ void __launch_bounds__(256) deflate_kernel(DeflateArgs a) {
+    // gated launch (the lane-order guards' retry pass of a batch with nothing else for this
+    // kernel): nothing to do while no guard has ever fired in this context
+    if (a.gate && a.guard[0] == 0 && a.guard[1] == 0) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
     for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];

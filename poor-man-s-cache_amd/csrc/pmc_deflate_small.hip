@@ -139,7 +139,7 @@ __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
 uint64_t deflate_front_wave_bytes(uint64_t n) { return front_layout(n).total; }
 // split-pipeline back (emission only): bytes | out | lcode | dcode | blcode | runs | lengths
 struct BackLayout {
-    uint64_t bytes, out, out_words, lcode, dcode, blcode, runs, ls, blfreq, total;
+    uint64_t bytes, out, out_words, lcode, dcode, blcode, runs, ls, blfreq, perm, total;
 };
 __host__ __device__ inline BackLayout back_layout(uint64_t n) {
     auto a = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
@@ -153,7 +153,8 @@ __host__ __device__ inline BackLayout back_layout(uint64_t n) {
     B.runs = B.blcode + 32 * 4;
     B.ls = B.runs + 320 * 2;
     B.blfreq = a(B.ls + kSplitRows); // scan_runs' bit-length counts (unused by the back)
-    B.total = B.blfreq + 32 * 4;
+    B.perm = B.blfreq + 32 * 4;      // the code-rank guard's symbols in canonical order (u16 per symbol)
+    B.total = a(B.perm + kSplitRows * 2);
     return B;
 }
 uint64_t deflate_back_wave_bytes(uint64_t n) { return back_layout(n).total; }
@@ -323,6 +324,9 @@ struct SmallWave {
     PMC_GLB uint32_t *tok;
     Trees *fb; // HBM scratch for the serial fallback
     PMC_LDS const uint32_t *crc_tab;
+    PMC_LDS uint16_t *perm; // split back: the code-rank guard's canonical order (BackLayout::perm)
+    uint32_t fault_rev = 0; // PMC_FAULT_LANE_ORDER builds: this value's sort takes its lanes in reverse
+    static constexpr uint64_t kBitsGuard = ~0ull; // emit_planned: the code-rank guard fired
     uint64_t st[16];
     uint64_t t_last;
     int stop; // PMC_STAMPS: end the value after phase `stop` (instruction-count attribution)
@@ -481,7 +485,11 @@ struct SmallWave {
             // lds_atomic_order.hip: 16.7M trials of skewed digit mixes, none out of order), so the
             // scatter stays stable without a ballot per digit bit (round 3: front 206 -> 191 ms)
             for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+#ifdef PMC_FAULT_LANE_ORDER // (diagnostic build: a chunk's positions in reverse lane order, which build_cn's guard must catch)
+                const uint32_t x = fault_rev ? c0 + 63u - l : c0 + l;
+#else
                 const uint32_t x = c0 + l;
+#endif
                 const uint32_t p = x < npos ? (pass ? (uint32_t)Tt[x] : x) : 0u;
                 const uint32_t d = (hash3(load4(p)) >> sh) & 255, hs = 16 * (d & 1);
                 if (x < npos) dst[(lds_add(&tab[d >> 1], 1u << hs) >> hs) & 0xffffu] = (uint16_t)p;
@@ -780,22 +788,31 @@ struct SmallWave {
     // CN[x] = chain candidates of x = entries before x in its run of the hash-sorted order,
     // less position 0 (zlib's NIL: head[] value 0 never starts a match; the sort is stable,
     // so position 0 is the first entry of its run).  HC = CN > 0 as bits.
+    // Returns 1 (uniform) when S is not the stable hash order: the sort's scatter slots come from
+    // returning LDS atomics whose same-word lanes are assumed to get their old values in lane order
+    // (measured on gfx950, not documented).  The guard checks what that order must produce -- (hash,
+    // position) strictly increasing along S -- and the caller sends the value to the retry kernel
+    // (per-lane counters, no atomic order) instead of parsing chains that may point forward.
     template <int PK>
-    __device__ __forceinline__ void build_cn(uint32_t npos, uint32_t k0) {
+    __device__ __forceinline__ uint32_t build_cn(uint32_t npos, uint32_t k0) {
         constexpr uint32_t RB = 16 - (PK > 0 ? PK : 0), CMAX = PK > 0 ? (1u << PK) - 1 : 255u;
         const uint32_t l = (uint32_t)lane_id();
         // has-candidate bits set by position below (HC as u32 words, LDS atomics): no second
         // pass over the positions
         for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
         wave_sync();
-        uint32_t ph = 0xffffffffu, prs = 0; // previous chunk's last hash and run start
+        uint32_t ph = 0xffffffffu, prs = 0, pq = 0; // previous chunk's last hash, run start, position
+        uint32_t bad = 0;
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
             const uint32_t k = c0 + l;
             const bool valid = k < npos;
             const uint32_t p = valid ? (uint32_t)S[k] : 0u;
             const uint32_t h = valid ? hash3(load4(p)) : 0xfffffffeu;
-            uint32_t hp = (uint32_t)__shfl_up((int)h, 1);
+            uint32_t hp = (uint32_t)__shfl_up((int)h, 1), pp = (uint32_t)__shfl_up((int)p, 1);
             hp = l == 0 ? ph : hp;
+            pp = l == 0 ? pq : pp;
+            // (hash, position) must increase: h > hp, or h == hp and p > pp (k = 0 has no predecessor)
+            bad |= (valid && k != 0 && (h < hp || (h == hp && p <= pp))) ? 1u : 0u;
             uint32_t rs = wave_incl_max_dpp(valid && h != hp ? k : 0u);
             rs = rs > prs ? rs : prs;
             const uint32_t cnt = k - rs - (rs == k0 && k > rs ? 1u : 0u);
@@ -806,8 +823,10 @@ struct SmallWave {
             }
             ph = readlane(h, 63);
             prs = readlane(rs, 63);
+            pq = readlane(p, 63);
         }
         wave_sync();
+        return ballot(bad != 0u) ? 1u : 0u;
     }
     // results of the current eval: window start p0, evaluated offsets m (uniform) and, in
     // lane j, best | q << 9 | cut << 31 for position p0 + j
@@ -1049,7 +1068,7 @@ struct SmallWave {
     __device__ __forceinline__ uint32_t parse_ondemand_body(uint32_t npos_, uint32_t len_, uint32_t k0_) {
         const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
         const uint32_t nw = (npos + 63) >> 6;
-        build_cn<PK>(npos, rfl(k0_));
+        if (sflag(build_cn<PK>(npos, rfl(k0_)))) return kNtokRetry; // (the sort's lane-order guard)
         stamp(11);
         PMC_STOP(13, 0)
         Group g;
@@ -1880,44 +1899,83 @@ struct SmallWave {
     // tmp[48 + tree * 16 + L] from one in-row DPP scan whose rows are the trees (96 words of tmp).
     // One call and one set of passes instead of three.  (round 3: ranks from returning atomics
     // instead of 6 ballots + a ds_bpermute per chunk)
-    __device__ __noinline__ void codes_from_lengths_all(PMC_LDS const uint8_t *Ls, PMC_LDS uint32_t *code0,
-                                                        PMC_LDS uint32_t *tmp) {
+    //
+    // Guard (returns 1, uniform, on failure): the ranks rest on the lane order of returning LDS
+    // atomics, measured on gfx950 but not documented.  Every symbol also lands at its canonical
+    // position -- (tree, shorter codes first, then rank) -- in perm[]; with the assumed order,
+    // the symbol one position before it, when it has the same length, is a smaller symbol.  A
+    // failure sends the value to the retry kernel instead of emitting codes assigned to the wrong
+    // symbols (a member that would only fail its CRC on GET).
+    // (PMC_FAULT_LANE_ORDER, a diagnostic build: lanes take the symbols of a chunk in reverse, the
+    // order the guard must catch)
+    __device__ __noinline__ uint32_t codes_from_lengths_all(PMC_LDS const uint8_t *Ls, PMC_LDS uint32_t *code0,
+                                                            PMC_LDS uint32_t *tmp, PMC_LDS uint16_t *perm) {
         constexpr int E = kLCodes + kDCodes + kBLCodes;
+        constexpr int NC = (E + 63) / 64;
         const uint32_t l = (uint32_t)lane_id();
+#ifdef PMC_FAULT_LANE_ORDER
+        const uint32_t lo = 63u - l;
+#else
+        const uint32_t lo = l;
+#endif
         for (uint32_t k = l; k < 96; k += 64) tmp[k] = 0;
         wave_sync();
         auto tree_of = [](int s) { return s < kLCodes ? 0u : s < kLCodes + kDCodes ? 1u : 2u; };
-        for (int c0 = 0; c0 < E; c0 += 64) {
-            const int s = c0 + (int)l;
+        uint32_t rk[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const int s = 64 * c + (int)lo;
             const bool in = s < E;
             const uint32_t len = in ? Ls[s] : 0u, t = tree_of(s), key = t << 4 | len;
             // the symbol's rank among the earlier ones of its (tree, length): one returning LDS
             // atomic (the lanes of one instruction get their old counts in lane order, and one
             // wave's atomics apply in order across chunks; scripts/micro/lds_atomic_order.hip)
-            if (in) code0[s + 2 * t] = len ? lds_add(&tmp[key], 1u) : 0u; // (slots: s, 288 + s - 286, 320 + s - 316)
+            rk[c] = in && len ? lds_add(&tmp[key], 1u) : 0u;
         }
         wave_sync();
         {
-            const uint32_t L = l & 15u, y = (L && l < 48) ? tmp[l] << (16 - L) : 0u;
-            uint32_t v = y;
+            const uint32_t L = l & 15u, cnt = (L && l < 48) ? tmp[l] : 0u, y = cnt << (16 - L);
+            uint32_t v = y, u = cnt;
             v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+            u += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x111, 0xf, 0xf, false);
             v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+            u += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x112, 0xf, 0xf, false);
             v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+            u += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x114, 0xf, 0xf, false);
             v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+            u += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x118, 0xf, 0xf, false);
             const uint32_t nc = (v - y) >> (16 - L);
             wave_sync();
-            if (l < 48 && L >= 1) tmp[48 + l] = nc;
-        }
-        wave_sync();
-        for (int c0 = 0; c0 < E; c0 += 64) {
-            const int s = c0 + (int)l;
-            if (s < E) {
-                const uint32_t len = Ls[s], t = tree_of(s), slot = (uint32_t)s + 2 * t;
-                const uint32_t mycode = tmp[48 + (t << 4 | len)] + code0[slot];
-                code0[slot] = len ? ((__builtin_bitreverse32(mycode) >> (32 - len)) | (len << 16)) : 0u;
+            if (l < 48 && L >= 1) {
+                tmp[48 + l] = nc;
+                tmp[96 + l] = u - cnt; // symbols of this tree with shorter codes
             }
         }
         wave_sync();
+        uint32_t pj[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const int s = 64 * c + (int)lo;
+            pj[c] = 0;
+            if (s < E) {
+                const uint32_t len = Ls[s], t = tree_of(s), slot = (uint32_t)s + 2 * t, key = t << 4 | len;
+                const uint32_t mycode = tmp[48 + key] + rk[c];
+                code0[slot] = len ? ((__builtin_bitreverse32(mycode) >> (32 - len)) | (len << 16)) : 0u;
+                // canonical position, 1-based (0: no code); trees at perm 0 / 286 / 316
+                pj[c] = len ? (uint32_t)(t == 0 ? 0 : t == 1 ? kLCodes : kLCodes + kDCodes) + tmp[96 + key] + rk[c] + 1
+                            : 0u;
+                if (len) perm[pj[c] - 1] = (uint16_t)s;
+            }
+        }
+        wave_sync();
+        uint32_t bad = 0;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const int s = 64 * c + (int)lo;
+            // rank > 0: the previous canonical position holds this (tree, length)'s previous symbol
+            if (pj[c] && rk[c]) bad |= perm[pj[c] - 2] >= (uint32_t)s ? 1u : 0u;
+        }
+        return ballot(bad != 0u) ? 1u : 0u;
     }
     // the block as planned by deflate_trees_kernel: plan = type | l_max << 2 | d_max << 11 |
     // max_blindex << 16 (type 0 stored, 1 fixed, 2 dynamic); Ls = lit/len, dist, bl lengths
@@ -1950,7 +2008,7 @@ struct SmallWave {
         } else {
             const int l_max = (int)((plan >> 2) & 511), d_max = (int)((plan >> 11) & 31), mbi = (int)((plan >> 16) & 31);
             // (lcode | dcode | blcode contiguous; runs is free scratch in the split back)
-            codes_from_lengths_all(Ls, lcode, (PMC_LDS uint32_t *)runs);
+            if (sflag(codes_from_lengths_all(Ls, lcode, (PMC_LDS uint32_t *)runs, perm))) return kBitsGuard;
             PMC_STOP(23, bitpos)
             const int lcodes = l_max + 1, dcodes = d_max + 1, blcodes = mbi + 1;
             if (l == 0) {
@@ -2046,6 +2104,7 @@ struct SmallWave {
                    : cnp < 0  ? parse_ondemand<-1>(npos, len, k0)
                               : parse_ondemand<0>(npos, len, k0);
             PMC_STOP(14, 0)
+            if (sflag(ntok == kNtokRetry ? 1u : 0u)) return kNtokRetry; // (sort guard: no histogram)
         } else {
             lit_run(0, 0, len);
             ntok = len;
@@ -2073,6 +2132,7 @@ struct SmallWave {
         wave_sync();
         stamp(0);
         uint64_t bitpos = emit_planned(ntok, len, 80, plan, Ls);
+        if (bitpos == kBitsGuard) return kDeflateRetry; // (the code-rank guard: the HBM kernel redoes it)
         PMC_STOP(23, 0)
         PMC_STOP(24, 0)
         PMC_STOP(25, 0)
@@ -2129,6 +2189,9 @@ struct SmallWave {
         uint32_t ntok;
         if (npos) {
             ntok = parse_ondemand<false>(npos, len, (uint32_t)R[0]);
+            // (sort_positions' per-lane counters are stable by construction, so the guard in
+            // build_cn cannot fire here; if it ever did, the HBM kernel redoes the value)
+            if (sflag(ntok == kNtokRetry ? 1u : 0u)) return kDeflateRetry;
         } else { // no position with MIN_MATCH lookahead: all literals
             lit_run(0, 0, len);
             ntok = len;
@@ -2278,6 +2341,7 @@ __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
             if (l == 0) {
                 a.rc[v] = rc;
                 if (rc) a.dst_len[v] = 0;
+                if (rc == kDeflateRetry) atomicAdd(a.guard, 1u);
             }
         }
     }

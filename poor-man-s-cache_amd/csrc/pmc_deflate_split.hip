@@ -64,7 +64,18 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
             const uint64_t v = g + (uint64_t)jj, gv = a.first + v;
             const uint32_t len = readlane(myl, jj);
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
+#ifdef PMC_FAULT_LANE_ORDER // (odd values fail the sort's guard; the even ones reach the back's code-rank guard)
+            w.fault_rev = (uint32_t)(gv & 1);
+#endif
             const uint32_t ntok = w.run_front(a.src + a.src_off[gv], len);
+            if (ntok == kNtokRetry) { // the sort's lane-order guard fired: the HBM kernel redoes the value
+                if (l == 0) {
+                    a.cN[v] = kNtokRetry;
+                    a.cZ[v] = 0;
+                    atomicAdd(a.guard, 1u);
+                }
+                continue;
+            }
             // histograms -> column v of the chunk's interleaved u16 table
             uint32_t nz = 0;
             for (int s = l; s < kLCodes + kDCodes; s += 64) {
@@ -362,7 +373,7 @@ template <int CAP>
 __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC_LDS uint32_t *col,
                             PMC_LDS uint16_t *aux) {
     const uint32_t len = a.src_len[a.first + v];
-    if (len == 0 || len <= a.min_len || len > a.lds_max_len || a.cN[v] == kNtokMultiBlock) return;
+    if (len == 0 || len <= a.min_len || len > a.lds_max_len || a.cN[v] >= kNtokRetry) return;
     LaneTrees<CAP> t;
     t.hp = col;
     t.blc = aux;
@@ -385,7 +396,9 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC
         typedef uint32_t v4u __attribute__((ext_vector_type(4)));
         PMC_GLB const v4u *g4 = (PMC_GLB const v4u *)t.hist;
         static_assert(kLCodes * 2 == 35 * 16 + 12 && kDCodes == 30, "distance row at v4u 35, byte 12");
-        static_assert(CAP >= 75, "heap slots 60..74 hold the staged distance frequencies");
+        // (stage_row below also fills heap slots 0..79 with the 20 x 16-byte lengths row, and the
+        // column has CAP + 1 slots before the blc / blf region)
+        static_assert(CAP >= 79, "heap slots 60..74 hold the staged distance frequencies, 0..79 the lengths row");
         v4u d5[5];
 #pragma unroll
         for (int i = 0; i < 5; i++) d5[i] = g4[35 + i];
@@ -463,6 +476,7 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
     w.blcode = to_lds<uint32_t>(base + B.blcode);
     w.runs = to_lds<uint16_t>(base + B.runs);
     w.blfreq = to_lds<uint32_t>(base + B.blfreq);
+    w.perm = to_lds<uint16_t>(base + B.perm);
     // (run_back touches only the arrays above; the rest of w still points into the larger
     // small_layout and must stay unused here)
     PMC_LDS uint8_t *Ls = to_lds<uint8_t>(base + B.ls); // code lengths from the trees kernel
@@ -501,7 +515,7 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
                 const uintptr_t sa = (uintptr_t)(a.src + readlane64(myo, j2)), ta = (uintptr_t)(a.cT + v2 * a.cap_len),
                                 la = (uintptr_t)(a.cL + v2 * kSplitRows);
                 const uint32_t ns = (uint32_t)(((sa & 127) + len2 + 127) >> 7),
-                               nt = n2 == kNtokMultiBlock ? 0u : (uint32_t)(((ta & 127) + 4ull * n2 + 127) >> 7),
+                               nt = n2 >= kNtokRetry ? 0u : (uint32_t)(((ta & 127) + 4ull * n2 + 127) >> 7),
                                nl = (uint32_t)(((la & 127) + kSplitRows + 127) >> 7);
                 const uint32_t k = (uint32_t)l;
                 const uintptr_t addr = k < ns ? (sa & ~(uintptr_t)127) + 128ull * k
@@ -517,7 +531,7 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
                 continue;
             }
             const uint32_t ntok = readlane(myn, j), plan = readlane(myp, j);
-            if (ntok == kNtokMultiBlock) {
+            if (ntok >= kNtokRetry) { // several blocks, or the sort's guard fired: the HBM kernel
                 if (l == 0) a.rc[gv] = kDeflateRetry;
                 continue;
             }
@@ -532,6 +546,7 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
             if (l == 0) {
                 a.rc[gv] = rc;
                 if (rc) a.dst_len[gv] = 0;
+                if (rc == kDeflateRetry) atomicAdd(a.guard + 1, 1u); // (the code-rank guard fired)
             }
             asm volatile("" ::"v"(pf));
         }

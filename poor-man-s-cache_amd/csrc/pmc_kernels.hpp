@@ -57,10 +57,17 @@ struct DeflateArgs {
     uint64_t min_len;
     int32_t retry;
     uint32_t front_batch; // split front: values per work-counter grab (>= 1)
+    // lane-order guard counters (context-lifetime, device): [0] values whose hash sort failed the
+    // (hash, position) order check, [1] values whose canonical-code ranks failed theirs.  Such a
+    // value is redone by the HBM kernel (retry), which the host launches gated: with `gate` set
+    // it returns at once while both counters are 0.
+    uint32_t *guard;
+    int32_t gate;
 };
 
 constexpr int32_t kDeflateRetry = -7778;     // internal rc: the split pipeline declined the value
 constexpr uint32_t kNtokMultiBlock = 0xffffffffu; // cN marker: >= 16383 symbols
+constexpr uint32_t kNtokRetry = 0xfffffffeu;      // cN marker: the sort's lane-order guard fired (retry)
 
 constexpr uint32_t kBackTabBytes = 8 * 256 * 4; // the back kernel's slicing-by-8 CRC tables (LDS per block)
 constexpr uint32_t kSplitRows = 336;  // 286 lit/len + 30 dist + 19 bit-length (+1)
@@ -138,6 +145,7 @@ __global__ void inflate_rec_kernel(InflateArgs a);
 __global__ void inflate_verify_kernel(InflateArgs a);
 __global__ void arg_check_kernel(const uint32_t *src_len, uint64_t n, uint64_t max_len, int32_t *rc,
                                  uint32_t *dst_len);
+__global__ void lane_order_probe_kernel(uint32_t trials, uint32_t *violations);
 __global__ void crc32_batch_kernel(const uint8_t *buf, const uint64_t *off, const uint32_t *len, uint64_t n,
                                    uint32_t *crc);
 

@@ -82,6 +82,35 @@ __global__ void arg_check_kernel(const uint32_t *src_len, uint64_t n, uint64_t m
         }
 }
 
+// Context self-test of the one undocumented hardware behaviour the compressor leans on: the lanes
+// of one ds_add_rtn_u32 that hit the same LDS word get their old values in lane order (the hash
+// sort's scatter and the canonical-code ranks).  Every trial packs two u16 counters per word as
+// the sort's table does; a lane's returned count must equal the number of lower lanes with its
+// digit.  pmc_ctx_create runs it once; on any violation the context compresses through the
+// kernels that do not depend on it (scripts/micro/lds_atomic_order.hip is the larger probe).
+__global__ void __launch_bounds__(256) lane_order_probe_kernel(uint32_t trials, uint32_t *violations) {
+    __shared__ uint32_t tab[4][128];
+    const int w = threadIdx.x / 64, l = lane_id();
+    uint32_t bad = 0;
+    for (uint32_t t = 0; t < trials; t++) {
+        for (int k = l; k < 128; k += 64) tab[w][k] = 0;
+        wave_sync();
+        uint32_t x = (uint32_t)(blockIdx.x * 7919u + w * 104729u + t * 31u) * 2654435761u + (uint32_t)l * 40503u;
+        x ^= x >> 13;
+        x *= 0x5bd1e995u;
+        x ^= x >> 15;
+        const uint32_t alpha = 1u + (t % 7 == 0 ? 255u : t % 9); // 1..256 digits, skewed to few
+        const uint32_t d = (x % alpha) & 255u;
+        const uint32_t old = lds_add(to_lds<uint32_t>(&tab[w][d >> 1]), 1u << (16 * (d & 1)));
+        const uint32_t r = (old >> (16 * (d & 1))) & 0xffffu;
+        uint32_t want = 0;
+        for (int j = 0; j < 64; j++) want += (j < l && (uint32_t)__shfl((int)d, j) == d) ? 1u : 0u;
+        bad += r != want ? 1u : 0u;
+        wave_sync();
+    }
+    if (bad) atomicAdd(violations, bad);
+}
+
 __global__ void isize_kernel(const uint8_t *src, const uint64_t *off, const uint32_t *len, uint32_t n, uint32_t *isz) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t L = len[i];

@@ -88,6 +88,7 @@ SIGNATURES = {
     "pmc_debug_stamps": (_c.c_int, [_p, _p]),
     "pmc_ctx_profile": (_c.c_int, [_p, _c.c_int]),
     "pmc_ctx_kernel_times": (_c.c_int, [_p, _c.POINTER(_c.c_double), _c.POINTER(_u32), _c.c_int]),
+    "pmc_ctx_guard_counts": (_c.c_int, [_p, _c.POINTER(_u32)]),
 }
 
 # pmc_ctx_kernel_times kinds (include/pmc_codec.h PMC_K_*)
@@ -176,6 +177,14 @@ class Context:
         if rc != 0:
             raise CodecUnavailable(f"pmc_ctx_kernel_times failed ({rc}): {last_error()}")
         return {KERNEL_KINDS[k]: (ms[k], cnt[k]) for k in range(n) if cnt[k]}
+
+    def guard_counts(self):
+        """Lane-order guard counters {sort, codes, probe} (include/pmc_codec.h pmc_ctx_guard_counts)."""
+        c = (_u32 * 3)()
+        rc = lib().pmc_ctx_guard_counts(self.handle, c)
+        if rc != 0:
+            raise CodecUnavailable(f"pmc_ctx_guard_counts failed ({rc}): {last_error()}")
+        return {"sort": c[0], "codes": c[1], "probe": c[2]}
 
     def close(self):
         if self.handle:
