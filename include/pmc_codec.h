@@ -74,7 +74,9 @@ uint32_t pmc_gzip_isize(const void *in, size_t in_len);
  * Value i occupies src[src_off[i] .. src_off[i]+src_len[i]); its gzip member is written to
  * dst[dst_off[i] ..), at most dst_cap[i] bytes, its length to dst_len[i] and its status to
  * rc[i].  All arrays are device pointers; the call only enqueues work on `stream`
- * (hipStream_t, NULL = legacy default stream) and returns.  max_len is an upper bound on
+ * (hipStream_t, NULL = legacy default stream) and returns -- except that a compress call whose
+ * max_len exceeds the split pipeline's limit (~31.8 KB) reads the number and lengths of its large
+ * values back to plan their scratch, so it waits for the stream up to that point.  max_len is an upper bound on
  * src_len[] (for compress) or on the decompressed sizes (for decompress); it selects the
  * kernel variant (LDS-resident vs HBM-resident working set).  Compress: a value with
  * src_len[i] > max_len is not compressed; it gets rc[i] = PMC_E_ARG, dst_len[i] = 0
@@ -281,7 +283,9 @@ int pmc_debug_stamps(pmc_ctx *ctx, uint64_t *dev_buf);
 #define PMC_K_INFLATE_VERIFY 8 /* CRC-32 check of the fast path's output               */
 #define PMC_K_ORDER 9          /* lane visit-order counting sorts (trees, lane inflate)  */
 #define PMC_K_INFLATE_REC 10   /* two-phase record decode of members up to 4 KiB output */
-#define PMC_K_COUNT 11
+#define PMC_K_DEFLATE_LARGE 11 /* large values: hash sort, segment parses, stitching     */
+#define PMC_K_DEFLATE_LARGE_EMIT 12 /* large values: blocks of the stitched tokens      */
+#define PMC_K_COUNT 13
 int pmc_ctx_profile(pmc_ctx *ctx, int enable);
 int pmc_ctx_kernel_times(pmc_ctx *ctx, double *ms, uint32_t *launches, int nkinds);
 
@@ -292,8 +296,10 @@ int pmc_ctx_kernel_times(pmc_ctx *ctx, double *ms, uint32_t *launches, int nkind
  * that fails is recompressed by the HBM kernel, which does not rely on it, so output stays
  * bit-exact.  Synchronizes the device and copies out the context's counters: counts[0] values
  * whose sort failed the check, counts[1] values whose code ranks failed it, counts[2] violations
- * in pmc_ctx_create's self-test (nonzero: the context compresses through the single-kernel path). */
-int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[3]);
+ * in pmc_ctx_create's self-test (nonzero: the context compresses through the single-kernel path),
+ * counts[3] values the other paths handed to the HBM kernel (31.8 KB-class values of several
+ * DEFLATE blocks; large values whose segment parses did not stitch). */
+int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[4]);
 
 #ifdef __cplusplus
 }

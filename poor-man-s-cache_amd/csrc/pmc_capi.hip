@@ -172,9 +172,12 @@ struct pmc_ctx {
     DevBuf order;                // inflate: lane visit order (bins | member indices)
     DevBuf recs;                 // inflate: the record kernel's per-lane record rows
     // lane-order guards (DeflateArgs::guard): u32 [0] sort, [1] code ranks, [2] the create-time probe's
-    // violations; lane_order_ok = the probe passed (else compress takes the kernels that do not need it)
+    // violations, [3] values sent to the HBM kernel's retry pass by the other paths; lane_order_ok = the probe passed (else compress takes the kernels that do not need it)
     DevBuf guard;
     bool lane_order_ok = true;
+    // large values (pmc_deflate_large.hip): selection list, round tables, round scratch, emit scratch
+    DevBuf lvsel, lvtab, lvbuf, lvemit;
+    HostBuf lvpin;
     // per direction (0 compress, 1 decompress): the event recorded after the last batch call and its
     // stream; a call on another stream waits for it, since both use the direction's scratch
     hipEvent_t dir_ev[2] = {};
@@ -387,11 +390,11 @@ PMC_API int pmc_ctx_create(int device, pmc_ctx **out) {
     return PMC_OK;
 }
 
-PMC_API int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[3]) {
+PMC_API int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[4]) {
     if (!ctx || !counts) return PMC_E_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(counts, ctx->guard.p, 12, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(counts, ctx->guard.p, 16, hipMemcpyDeviceToHost));
     return PMC_OK;
 }
 
@@ -406,6 +409,11 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     c->crcx.release();
     c->recs.release();
     c->guard.release();
+    c->lvsel.release();
+    c->lvtab.release();
+    c->lvbuf.release();
+    c->lvemit.release();
+    c->lvpin.release();
     for (auto &r : c->krecs) {
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
@@ -456,6 +464,153 @@ PMC_API uint32_t pmc_gzip_isize(const void *in, size_t in_len) {
 // pays once a batch fills the CUs.
 constexpr uint32_t kLatencyBatch = 64;
 
+// ---- large values (pmc_deflate_large.hip) ------------------------------------------------------------
+// The batch's values of lo < len <= hi.  Their lengths live on the device: one small readback (a count,
+// then the (index, length) list) lets the host plan rounds of values whose sort arrays, token buffers
+// and state maps fit a scratch budget.  This is the only synchronous step of a device-resident compress
+// call, taken only when max_len says such values may be present.
+static int large_values(pmc_ctx *ctx, const DeflateArgs &a, uint64_t lo, uint64_t hi, hipStream_t st) {
+    const uint64_t n = a.n;
+    int r = ctx->lvsel.ensure(8 + 8 * n);
+    if (r) return r;
+    uint32_t *sel = (uint32_t *)ctx->lvsel.p;
+    HIP_TRY(hipMemsetAsync(sel, 0, 8, st));
+    hipLaunchKernelGGL(lv_select_kernel, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, st,
+                       a.src_len, n, lo, hi, sel);
+    uint32_t cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, sel, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (!cnt) return PMC_OK;
+    std::vector<uint32_t> list(2 * (size_t)cnt);
+    HIP_TRY(hipMemcpy(list.data(), sel + 2, 8 * (size_t)cnt, hipMemcpyDeviceToHost));
+    std::vector<std::pair<uint32_t, uint32_t>> vals(cnt);
+    for (uint32_t k = 0; k < cnt; k++) vals[k] = {list[2 * k], list[2 * k + 1]};
+    std::sort(vals.begin(), vals.end());
+    auto nseg_of = [](uint64_t len) { return std::max<uint64_t>(1, len / kLvSeg); };
+    auto nch_of = [](uint64_t len) { return (len - 2 + kLvChunk - 1) / kLvChunk; };
+    auto tok_of = [&](uint64_t len) { // token capacity of the value's segments
+        const uint64_t ns = nseg_of(len);
+        return (ns - 1) * (kLvSeg + kLvOverlap + 2) + (len - (ns - 1) * kLvSeg) + 2;
+    };
+    auto bytes_of = [&](uint64_t len) {
+        return 13 * (len - 2) + 4 * tok_of(len) + nseg_of(len) * (2 * kLvOverlap * 4 + 16) + nch_of(len) * 1024 + 64;
+    };
+    auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
+    const uint64_t budget = 24ull << 30;
+    size_t v0 = 0;
+    while (v0 < vals.size()) {
+        // one round: values v0 .. v1 - 1
+        size_t v1 = v0;
+        uint64_t need = 0, P = 0, nseg = 0, nch = 0, maxlen = 0;
+        while (v1 < vals.size() && (v1 == v0 || need + bytes_of(vals[v1].second) <= budget)) {
+            const uint64_t len = vals[v1].second;
+            need += bytes_of(len);
+            P += len - 2;
+            nseg += nseg_of(len);
+            nch += nch_of(len);
+            maxlen = std::max(maxlen, len);
+            v1++;
+        }
+        const uint32_t nv = (uint32_t)(v1 - v0);
+        // host tables, in the order of the device table buffer
+        const uint64_t o_val = 0, o_pb = al(o_val + 4ull * nv), o_seg0 = al(o_pb + 8ull * nv),
+                       o_ch0 = al(o_seg0 + 4ull * (nv + 1)), o_sval = al(o_ch0 + 4ull * (nv + 1)),
+                       o_stok = al(o_sval + 4 * nseg), o_cval = al(o_stok + 8 * nseg), tab_bytes = al(o_cval + 4 * nch);
+        HIP_TRY(hipStreamSynchronize(st)); // (the previous round's kernels read the pinned tables' device copy)
+        r = ctx->lvpin.ensure(tab_bytes);
+        if (!r) r = ctx->lvtab.ensure(tab_bytes);
+        if (r) return r;
+        uint8_t *h = (uint8_t *)ctx->lvpin.p;
+        uint32_t *t_val = (uint32_t *)(h + o_val), *t_seg0 = (uint32_t *)(h + o_seg0), *t_ch0 = (uint32_t *)(h + o_ch0),
+                 *t_sval = (uint32_t *)(h + o_sval), *t_cval = (uint32_t *)(h + o_cval);
+        uint64_t *t_pb = (uint64_t *)(h + o_pb), *t_stok = (uint64_t *)(h + o_stok);
+        uint64_t pb = 0, tb = 0;
+        uint32_t sg = 0, ch = 0;
+        for (uint32_t ov = 0; ov < nv; ov++) {
+            const uint64_t len = vals[v0 + ov].second, ns = nseg_of(len), nc = nch_of(len);
+            t_val[ov] = vals[v0 + ov].first;
+            t_pb[ov] = pb;
+            t_seg0[ov] = sg;
+            t_ch0[ov] = ch;
+            for (uint64_t j = 0; j < ns; j++, sg++) {
+                t_sval[sg] = ov;
+                t_stok[sg] = tb;
+                tb += j + 1 < ns ? kLvSeg + kLvOverlap + 2 : len - j * kLvSeg + 2;
+            }
+            for (uint64_t c = 0; c < nc; c++, ch++) t_cval[ch] = ov;
+            pb += len - 2;
+        }
+        t_seg0[nv] = sg;
+        t_ch0[nv] = ch;
+        uint8_t *dt = (uint8_t *)ctx->lvtab.p;
+        HIP_TRY(hipMemcpyAsync(dt, h, tab_bytes, hipMemcpyHostToDevice, st));
+        // round scratch: tmp | S | R | HC | hist | tok | map | seg_tok | fail
+        const uint64_t b_tmp = 0, b_S = al(b_tmp + 4 * P), b_R = al(b_S + 4 * P), b_HC = al(b_R + 4 * P),
+                       b_hist = al(b_HC + P), b_tok = al(b_hist + 1024 * nch), b_map = al(b_tok + 4 * tb),
+                       b_stok = al(b_map + 2ull * kLvOverlap * 4 * nseg), b_fail = al(b_stok + 16 * nseg),
+                       scratch = al(b_fail + 4ull * nv);
+        r = ctx->lvbuf.ensure(scratch);
+        if (r) return r;
+        uint8_t *d = (uint8_t *)ctx->lvbuf.p;
+        LargeArgs L{};
+        L.src = a.src;
+        L.src_off = a.src_off;
+        L.src_len = a.src_len;
+        L.lv_val = (const uint32_t *)(dt + o_val);
+        L.lv_pbase = (const uint64_t *)(dt + o_pb);
+        L.lv_seg0 = (const uint32_t *)(dt + o_seg0);
+        L.lv_ch0 = (const uint32_t *)(dt + o_ch0);
+        L.seg_val = (const uint32_t *)(dt + o_sval);
+        L.seg_tok0 = (const uint64_t *)(dt + o_stok);
+        L.ch_val = (const uint32_t *)(dt + o_cval);
+        L.nv = nv;
+        L.nseg = (uint32_t)nseg;
+        L.nch = (uint32_t)nch;
+        L.tmp = (uint32_t *)(d + b_tmp);
+        L.S = (uint32_t *)(d + b_S);
+        L.R = (uint32_t *)(d + b_R);
+        L.HC = d + b_HC;
+        L.hist = (uint32_t *)(d + b_hist);
+        L.tok = (uint32_t *)(d + b_tok);
+        L.map = (uint32_t *)(d + b_map);
+        L.seg_tok = (uint32_t *)(d + b_stok);
+        L.fail = (int32_t *)(d + b_fail);
+        const unsigned cb = (unsigned)std::min<uint64_t>((nch + 3) / 4, (uint64_t)ctx->cus * 8);
+        const unsigned sb = (unsigned)std::min<uint64_t>((nseg + 3) / 4, (uint64_t)ctx->cus * 8);
+        const unsigned vb = (unsigned)std::min<uint64_t>(nv, (uint64_t)ctx->cus * 4);
+        klaunch(ctx, PMC_K_DEFLATE_LARGE, st, [&] {
+            for (int pass = 0; pass < 2; pass++) {
+                hipLaunchKernelGGL(lv_sort_hist_kernel, dim3(cb), dim3(256), 0, st, L, pass);
+                hipLaunchKernelGGL(lv_sort_scan_kernel, dim3(vb), dim3(256), 0, st, L);
+                hipLaunchKernelGGL(lv_sort_scatter_kernel, dim3(cb), dim3(256), 0, st, L, pass);
+            }
+            hipLaunchKernelGGL(lv_rank_kernel, dim3(cb), dim3(256), 0, st, L);
+            hipLaunchKernelGGL(lv_parse_kernel, dim3(sb), dim3(256), 0, st, L);
+            hipLaunchKernelGGL(lv_stitch_kernel, dim3(vb), dim3(64), 0, st, L);
+        });
+        // emit: one wave per value
+        DeflateArgs e = a;
+        e.cap_len = maxlen;
+        e.wave_bytes = deflate_lv_emit_wave_bytes(maxlen);
+        const uint64_t ew = std::max<uint64_t>(4, std::min<uint64_t>(
+            {(uint64_t)(nv + 3) / 4 * 4, (uint64_t)ctx->cus * 4, std::max<uint64_t>(4, (8ull << 30) / e.wave_bytes / 4 * 4)}));
+        r = ctx->lvemit.ensure(ew * e.wave_bytes);
+        if (r) return r;
+        e.scratch = (uint8_t *)ctx->lvemit.p;
+        klaunch(ctx, PMC_K_DEFLATE_LARGE_EMIT, st, [&] {
+            hipLaunchKernelGGL(deflate_lv_emit_kernel, dim3((unsigned)(ew / 4)), dim3(256), deflate_lv_emit_lds(4), st, e,
+                               L);
+        });
+        hipError_t err = hipGetLastError();
+        if (err != hipSuccess) {
+            set_err("large-value kernels", err);
+            return PMC_E_NO_DEVICE;
+        }
+        v0 = v1;
+    }
+    return PMC_OK;
+}
+
 static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
                                uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap,
                                uint32_t *dst_len, int32_t *rc, uint32_t max_len, void *stream,
@@ -499,19 +654,24 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     const uint64_t big_hi = big_pass ? std::min<uint64_t>(big_lim, max_len) : 0;
     const uint64_t big_cap = big_pass ? std::min<uint64_t>((big_hi + 63) & ~(uint64_t)63, big_lim) : 0;
     const uint64_t hbm_cut = big_pass ? big_hi : lds_cut; // the HBM kernel takes lengths above this
+    // values above hbm_cut: the large-value path (pmc_deflate_large.hip), except on the V1 A/B path
+    const bool lv = !force_v1 && max_len > hbm_cut;
     uint64_t hbm_waves = 0, hbm_wb = deflate_wave_bytes(true, max_len);
-    // without values for the HBM kernel it still runs, gated, as the lane-order guards' retry pass:
-    // it returns at once while no guard has fired in this context
-    const bool gated = !(max_len > hbm_cut || big_pass);
+    // The HBM kernel takes values by length only on the V1 path.  Otherwise it runs gated, as the retry
+    // pass of the values the other paths declined (a lane-order guard fired, a large-pass value of
+    // several blocks, a large value whose segments did not stitch): it returns at once while the
+    // context's counters of those are 0.
+    const bool gated = !(force_v1 && max_len > hbm_cut);
     if (!gated) {
         // as many waves as the kernel's 196 VGPRs let a CU hold (2 per SIMD) within a 32 GiB scratch
         // budget: at 2 waves per CU (round 1-2) the latency-bound walk left 64 KiB values at
         // 0.52 GiB/s
         hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 8,
                                                              (32ull << 30) / std::max<uint64_t>(hbm_wb, 1)));
-    } else {
-        // (the single-kernel path's sort and codes do not use returning-atomic ranks: no retry pass)
-        hbm_waves = split ? (uint64_t)ctx->cus : 0;
+    } else if (split || lv) {
+        // (the single-kernel path's sort and codes do not use returning-atomic ranks: no retry pass
+        // unless large values ran)
+        hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>(64, (4ull << 30) / std::max<uint64_t>(hbm_wb, 1)));
     }
     hbm_waves = std::min<uint64_t>(hbm_waves, n);
     if (split) {
@@ -662,10 +822,15 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
         }
     }
     a.tokens = (uint32_t *)ctx->tokens.p;
-    // ---- HBM kernel (values > lds_cut) ----
+    // ---- large values (> hbm_cut): segment-parallel parse, stitched, emitted per value ----
+    if (lv) {
+        const int r = large_values(ctx, a, hbm_cut, max_len, st);
+        if (r) return r;
+    }
+    // ---- HBM kernel (V1: values > lds_cut; else gated retries) ----
     if (hbm_waves) {
         a.cap_len = max_len;
-        a.lds_max_len = hbm_cut;
+        a.lds_max_len = gated ? max_len : hbm_cut;
         a.retry = 1; // (large-pass values of several blocks, and values a lane-order guard declined)
         a.gate = gated ? 1 : 0;
         a.wave_bytes = hbm_wb;

@@ -3,6 +3,7 @@
 #include "pmc_deflate.hip"
 #include "pmc_deflate_small.hip"
 #include "pmc_deflate_split.hip"
+#include "pmc_deflate_large.hip"
 #include "pmc_inflate.hip"
 #include "pmc_inflate_lane.hip"
 #include "pmc_inflate_rec.hip"

@@ -384,6 +384,97 @@ struct DeflateWave {
         return bitpos;
     }
 
+    // ---- large values: the stitched token stream of pmc_deflate_large.hip ----------------------------
+    // Blocks of 16383 symbols (zlib's lit_bufsize - 1: _tr_tally reports the flush at the 16383rd),
+    // then the rest (possibly none) as the last block, each through flush_block.  Histograms are
+    // counted by LDS atomics as the tokens are copied to the wave's slab; token positions follow from
+    // a prefix sum of their lengths.  `hist`: 320 u32 of LDS (lit/len | dist).
+    __device__ int run_lv(const uint8_t *src, uint64_t len, uint8_t *dst, uint32_t dst_cap, uint32_t *dst_len,
+                          const LargeArgs &L, uint32_t ov, PMC_LDS uint32_t *hist) {
+        const int l = lane_id();
+        const Tables &T = c_tables;
+        const uint32_t crc = wave_crc32(src, (uint32_t)len, crc_tab);
+        for (uint64_t k = l; k < out_words; k += 64) outw[k] = 0;
+        for (int k = l; k < 320; k += 64) hist[k] = 0;
+        sync();
+        if (l < 10) {
+            const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 2, 3};
+            outb[l] = hdr[l];
+        }
+        sync();
+        uint64_t bitpos = 80, pos = 0, block_start = 0, last_start = 0;
+        uint32_t ntok = 0;
+        auto flush = [&](bool last) {
+            // freqs -> the trees (init_block: END_BLOCK counted once)
+            for (int s = l; s < kLCodes; s += 64) tr->ltree[s].fc = (uint16_t)(s == kEndBlock ? 1u : hist[s]);
+            if (l < kDCodes) tr->dtree[l].fc = (uint16_t)hist[kLCodes + l];
+            if (l < kBLCodes) tr->bltree[l].fc = 0;
+            sync();
+            // the window base at the flush's loop top (fill_window's slides so far): a stored block needs
+            // its bytes still in the window (deflate.c _tr_flush_block's buf != NULL)
+            const uint64_t t = last ? len : last_start + 1;
+            uint64_t B = 0;
+            for (;;) {
+                const uint64_t wend = len < B + 2 * kWSize ? len : B + 2 * kWSize;
+                if (t - B >= kWSize + kMaxDist && t + kMinLookahead > wend) B += kWSize;
+                else break;
+            }
+            wave_sync_global(); // slab stores visible to the emitting lanes
+            bitpos = flush_block(ntok, block_start, pos, B, last, bitpos);
+            block_start = pos;
+            ntok = 0;
+            for (int k = l; k < 320; k += 64) hist[k] = 0;
+            sync();
+        };
+        const uint32_t g0 = L.lv_seg0[ov], g1 = L.lv_seg0[ov + 1];
+        for (uint32_t g = g0; g < g1; g++) {
+            const uint32_t *tk = L.tok + L.seg_tok0[g];
+            uint32_t t = L.seg_tok[(uint64_t)g * 4 + 1];
+            const uint32_t te = L.seg_tok[(uint64_t)g * 4 + 2];
+            while (t < te) {
+                uint32_t take = te - t < 64 ? te - t : 64;
+                take = take < kSymsPerBlock - ntok ? take : kSymsPerBlock - ntok;
+                const bool in = (uint32_t)l < take;
+                const uint32_t x = in ? tk[t + l] : 0u, dist = x >> 16, lc = x & 0xff;
+                if (in) {
+                    tok[ntok + l] = x;
+                    if (dist) {
+                        lds_add(&hist[T.length_code[lc] + kLiterals + 1], 1u);
+                        lds_add(&hist[kLCodes + d_code(T, dist - 1)], 1u);
+                    } else {
+                        lds_add(&hist[lc], 1u);
+                    }
+                }
+                const uint32_t tl = in ? (dist ? lc + kMinMatch : 1u) : 0u;
+                const uint32_t incl = wave_incl_scan_dpp(tl);
+                last_start = pos + readlane(incl - tl, (int)take - 1);
+                pos += readlane(incl, 63);
+                ntok += take;
+                t += take;
+                if (ntok == kSymsPerBlock) flush(false);
+            }
+        }
+        flush(true);
+        uint64_t nbytes = bitpos >> 3;
+        if (l < 8) {
+            uint32_t v = l < 4 ? crc : (uint32_t)len;
+            outb[nbytes + l] = (uint8_t)(v >> (8 * (l & 3)));
+        }
+        nbytes += 8;
+        sync();
+        if (nbytes > dst_cap || pos != len) return pos != len ? kDeflateRetry : PMC_E_CAPACITY_DEV;
+        if ((((uintptr_t)dst) & 3) == 0) {
+            uint32_t *d4 = reinterpret_cast<uint32_t *>(dst);
+            uint64_t full = nbytes >> 2;
+            for (uint64_t k = l; k < full; k += 64) d4[k] = outw[k];
+            if ((uint64_t)l < (nbytes & 3)) dst[full * 4 + l] = outb[full * 4 + l];
+        } else {
+            for (uint64_t k = l; k < nbytes; k += 64) dst[k] = outb[k];
+        }
+        if (l == 0) *dst_len = (uint32_t)nbytes;
+        return 0;
+    }
+
     // ---- one value -------------------------------------------------------------------------
     __device__ int run(const uint8_t *src, uint64_t len, uint8_t *dst, uint32_t dst_cap, uint32_t *dst_len) {
         const int l = lane_id();
@@ -509,7 +600,8 @@ template <bool kHbm>
 __global__ void __launch_bounds__(256) deflate_kernel(DeflateArgs a) {
     // gated launch (the lane-order guards' retry pass of a batch with nothing else for this
     // kernel): nothing to do while no guard has ever fired in this context
-    if (a.gate && a.guard[0] == 0 && a.guard[1] == 0) return;
+    // (guard[3]: large values the stitched path declined)
+    if (a.gate && a.guard[0] == 0 && a.guard[1] == 0 && a.guard[3] == 0) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
     for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
@@ -580,5 +672,49 @@ __global__ void __launch_bounds__(256) deflate_kernel(DeflateArgs a) {
 
 template __global__ void deflate_kernel<false>(DeflateArgs);
 template __global__ void deflate_kernel<true>(DeflateArgs);
+
+// ---- large values: one wave per value emits its stitched tokens (pmc_deflate_large.hip) -----------
+// Per wave: HBM scratch = the output image | the symbol slab; LDS = the Trees (zlib's heap and the
+// serial plan_block run on lane 0 against LDS, not HBM) | 320 histogram counters.
+constexpr uint64_t kLvTreesBytes = (sizeof(Trees) + 15) & ~(uint64_t)15;
+constexpr uint64_t kLvEmitLdsPerWave = kLvTreesBytes + 320 * 4;
+uint64_t deflate_lv_emit_wave_bytes(uint64_t n) { return align16(gzip_bound(n) + 16) + (uint64_t)kSlabSyms * 4; }
+uint64_t deflate_lv_emit_lds(int waves) { return 1024 + (uint64_t)waves * kLvEmitLdsPerWave; }
+
+__global__ void __launch_bounds__(256) deflate_lv_emit_kernel(DeflateArgs a, LargeArgs L) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
+    __syncthreads();
+    const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
+    const uint64_t wave = (uint64_t)blockIdx.x * wpb + wib, nwaves = (uint64_t)gridDim.x * wpb;
+    uint8_t *wl = lds + 1024 + (uint64_t)wib * kLvEmitLdsPerWave;
+    uint8_t *base = a.scratch + wave * a.wave_bytes;
+    DeflateWave<true> W;
+    W.tr = reinterpret_cast<Trees *>(wl);
+    W.out_words = align16(gzip_bound(a.cap_len) + 16) / 4;
+    W.outw = reinterpret_cast<uint32_t *>(base);
+    W.outb = base;
+    W.tok = reinterpret_cast<uint32_t *>(base + W.out_words * 4);
+    W.crc_tab = crc_tab;
+    for (int k = 0; k < 8; k++) W.st[k] = 0;
+    PMC_LDS uint32_t *hist = to_lds<uint32_t>(wl + kLvTreesBytes);
+    for (uint64_t ov = wave; ov < L.nv; ov += nwaves) {
+        const uint32_t v = L.lv_val[ov];
+        const uint64_t len = a.src_len[v];
+        int rc = kDeflateRetry;
+        if (!L.fail[ov]) {
+            W.b = const_cast<uint8_t *>(a.src + a.src_off[v]);
+            W.out_words = align16(gzip_bound(len) + 16) / 4;
+            rc = W.run_lv(a.src + a.src_off[v], len, a.dst + a.dst_off[v], a.dst_cap[v], a.dst_len + v, L, (uint32_t)ov,
+                          hist);
+        }
+        if (l == 0) {
+            a.rc[v] = rc;
+            if (rc) a.dst_len[v] = 0;
+            if (rc == kDeflateRetry) atomicAdd(a.guard + 3, 1u); // (the HBM kernel redoes the value)
+        }
+    }
+}
 
 } // namespace pmc

@@ -532,7 +532,10 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
             }
             const uint32_t ntok = readlane(myn, j), plan = readlane(myp, j);
             if (ntok >= kNtokRetry) { // several blocks, or the sort's guard fired: the HBM kernel
-                if (l == 0) a.rc[gv] = kDeflateRetry;
+                if (l == 0) {
+                    a.rc[gv] = kDeflateRetry;
+                    if (ntok == kNtokMultiBlock) atomicAdd(a.guard + 3, 1u); // (opens the gated retry pass)
+                }
                 continue;
             }
             { // the code-length row (336 B; rows and Ls are 16-byte aligned) as dwords

@@ -65,6 +65,42 @@ struct DeflateArgs {
     int32_t gate;
 };
 
+// ---- large values (pmc_deflate_large.hip): values above the split pipeline's large pass ---------------
+// Each value's positions are sorted stably by hash in HBM (S, and the rank array R), then cut into
+// segments of kLvSeg positions that one wave each parses speculatively from a fresh deflate_slow state
+// (on through kLvOverlap positions of the next segment); a parse is exact from the first loop-top
+// position where its state equals the exact parse of the segment before it (stitching), and one wave
+// per value then emits the stitched token stream block by block (deflate_lv_emit_kernel).
+constexpr uint32_t kLvSeg = 16384, kLvOverlap = 2048, kLvChunk = 4096;
+struct LargeArgs {
+    const uint8_t *src;
+    const uint64_t *src_off;
+    const uint32_t *src_len;
+    // round tables (host-planned, device copies)
+    const uint32_t *lv_val;   // [nv] batch index of large value ov
+    const uint64_t *lv_pbase; // [nv] base of its positions in S / R / HC / tmp
+    const uint32_t *lv_seg0;  // [nv + 1] first segment of each value
+    const uint32_t *lv_ch0;   // [nv + 1] first sort chunk of each value
+    const uint32_t *seg_val;  // [nseg] value ordinal
+    const uint64_t *seg_tok0; // [nseg] base of the segment's token buffer in tok
+    const uint32_t *ch_val;   // [nch] value ordinal of sort chunk c (chunk c - lv_ch0[ov] of the value)
+    uint32_t nv, nseg, nch;
+    uint32_t *tmp, *S, *R;    // position-indexed (lv_pbase): sort scratch, sorted positions, ranks
+    uint8_t *HC;              // position-indexed: the nearest chain candidate exists (zlib's search runs)
+    uint32_t *hist;           // [nch][256] digit counts -> scatter bases
+    uint32_t *tok;            // segment token buffers (literal = byte, match = dist << 16 | len - 3)
+    uint32_t *map;            // [nseg][2][kLvOverlap]: loop-top states of the start / continuation regions
+    uint32_t *seg_tok;        // [nseg][4]: tokens parsed, stitched begin, stitched end, (unused)
+    int32_t *fail;            // [nv] no convergence at some boundary: the HBM kernel redoes the value
+};
+__global__ void lv_select_kernel(const uint32_t *src_len, uint64_t n, uint64_t lo, uint64_t hi, uint32_t *out);
+__global__ void lv_sort_hist_kernel(LargeArgs a, int pass);
+__global__ void lv_sort_scan_kernel(LargeArgs a);
+__global__ void lv_sort_scatter_kernel(LargeArgs a, int pass);
+__global__ void lv_rank_kernel(LargeArgs a);
+__global__ void lv_parse_kernel(LargeArgs a);
+__global__ void lv_stitch_kernel(LargeArgs a);
+
 constexpr int32_t kDeflateRetry = -7778;     // internal rc: the split pipeline declined the value
 constexpr uint32_t kNtokMultiBlock = 0xffffffffu; // cN marker: >= 16383 symbols
 constexpr uint32_t kNtokRetry = 0xfffffffeu;      // cN marker: the sort's lane-order guard fired (retry)
@@ -130,6 +166,8 @@ uint64_t inflate_wave_bytes(bool hbm, uint64_t max_out, uint64_t max_in);
 
 template <bool kHbm>
 __global__ void deflate_kernel(DeflateArgs a);
+__global__ void deflate_lv_emit_kernel(DeflateArgs a, LargeArgs L);
+uint64_t deflate_lv_emit_wave_bytes(uint64_t n);
 __global__ void deflate_small_kernel(DeflateArgs a);
 uint64_t deflate_front_wave_bytes(uint64_t n);
 uint64_t deflate_back_wave_bytes(uint64_t n);

@@ -93,13 +93,15 @@ SIGNATURES = {
 
 # pmc_ctx_kernel_times kinds (include/pmc_codec.h PMC_K_*)
 KERNEL_KINDS = ["deflate_front", "deflate_trees", "deflate_back", "deflate_mono", "deflate_hbm", "inflate_lds",
-                "inflate_hbm", "inflate_lane", "inflate_verify", "order", "inflate_rec"]
+                "inflate_hbm", "inflate_lane", "inflate_verify", "order", "inflate_rec", "deflate_large",
+                "deflate_large_emit"]
 KERNEL_NAMES = {"deflate_front": "pmc::deflate_front_kernel", "deflate_trees": "pmc::deflate_trees_kernel",
                 "deflate_back": "pmc::deflate_back_kernel", "deflate_mono": "pmc::deflate_small_kernel",
                 "deflate_hbm": "pmc::deflate_kernel<true>", "inflate_lds": "pmc::inflate_kernel<false>",
                 "inflate_hbm": "pmc::inflate_kernel<true>", "inflate_lane": "pmc::inflate_lane_kernel",
                 "inflate_verify": "pmc::inflate_verify_kernel", "order": "pmc::order_{hist,scan,scatter}_kernel",
-                "inflate_rec": "pmc::inflate_rec_kernel"}
+                "inflate_rec": "pmc::inflate_rec_kernel", "deflate_large": "pmc::lv_*_kernel",
+                "deflate_large_emit": "pmc::deflate_lv_emit_kernel"}
 
 
 def lib():
@@ -179,12 +181,12 @@ class Context:
         return {KERNEL_KINDS[k]: (ms[k], cnt[k]) for k in range(n) if cnt[k]}
 
     def guard_counts(self):
-        """Lane-order guard counters {sort, codes, probe} (include/pmc_codec.h pmc_ctx_guard_counts)."""
-        c = (_u32 * 3)()
+        """Guard counters {sort, codes, probe, retry} (include/pmc_codec.h pmc_ctx_guard_counts)."""
+        c = (_u32 * 4)()
         rc = lib().pmc_ctx_guard_counts(self.handle, c)
         if rc != 0:
             raise CodecUnavailable(f"pmc_ctx_guard_counts failed ({rc}): {last_error()}")
-        return {"sort": c[0], "codes": c[1], "probe": c[2]}
+        return {"sort": c[0], "codes": c[1], "probe": c[2], "retry": c[3]}
 
     def close(self):
         if self.handle:

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4: the large-value path -- its parity tests, the guard tests, the codec suite's large cases,
+# then 40K x 64 KiB and 1000 x 1 MiB JSON-slice benches (compress + decompress, every value verified).
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+T=${TAG:-r4large}
+mkdir -p gpurun_out/$T
+timeout -k 10 300 python -u -m pytest tests/test_gpu_large.py -x -v --timeout 240 --timeout-method thread > gpurun_out/$T/pytest_large.txt 2>&1; rc=$?
+tail -5 gpurun_out/$T/pytest_large.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -m pytest tests/test_gpu_guard.py -x -v --timeout 240 --timeout-method thread > gpurun_out/$T/pytest_guard.txt 2>&1; rc=$?
+tail -3 gpurun_out/$T/pytest_guard.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u -m pytest tests/test_gpu_codec.py -x -v -k "golden or ragged or multi_megabyte" --timeout 240 --timeout-method thread > gpurun_out/$T/pytest_codec.txt 2>&1; rc=$?
+tail -3 gpurun_out/$T/pytest_codec.txt; [ $rc -eq 0 ] || exit $rc
+for cfg in "40000 65536" "1000 1048576" "100000 30000"; do
+  set -- $cfg
+  timeout -k 10 300 python bench.py --no-cpu-baseline --n $1 --vlen $2 --steps 2 > gpurun_out/$T/b_$2.json 2> gpurun_out/$T/b_$2.err || exit $?
+  python3 -c "import json;d=json.load(open('gpurun_out/$T/b_$2.json'));print('$2',d['value'],d['compress_gib_s'],d['decompress_gib_s'],d['mismatches'],d['roofline']['kernel_ms_per_step'])"
+done
