@@ -298,8 +298,10 @@ int pmc_ctx_kernel_times(pmc_ctx *ctx, double *ms, uint32_t *launches, int nkind
  * whose sort failed the check, counts[1] values whose code ranks failed it, counts[2] violations
  * in pmc_ctx_create's self-test (nonzero: the context compresses through the single-kernel path),
  * counts[3] values the other paths handed to the HBM kernel (31.8 KB-class values of several
- * DEFLATE blocks; large values whose segment parses did not stitch). */
-int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[4]);
+ * DEFLATE blocks; large values whose segment parses did not stitch), counts[4] members the
+ * decompress fast paths (record / lane kernels) handed to the wave-per-member kernels (stored or
+ * unusual blocks, and every error verdict). */
+int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[5]);
 
 #ifdef __cplusplus
 }

@@ -172,7 +172,8 @@ struct pmc_ctx {
     DevBuf order;                // inflate: lane visit order (bins | member indices)
     DevBuf recs;                 // inflate: the record kernel's per-lane record rows
     // lane-order guards (DeflateArgs::guard): u32 [0] sort, [1] code ranks, [2] the create-time probe's
-    // violations, [3] values sent to the HBM kernel's retry pass by the other paths; lane_order_ok = the probe passed (else compress takes the kernels that do not need it)
+    // violations, [3] values sent to the HBM kernel's retry pass by the other paths, [4] members the
+    // decompress fast paths handed to the wave kernels; lane_order_ok = the probe passed (else compress takes the kernels that do not need it)
     DevBuf guard;
     bool lane_order_ok = true;
     // large values (pmc_deflate_large.hip): selection list, round tables, round scratch, emit scratch
@@ -374,7 +375,7 @@ PMC_API int pmc_ctx_create(int device, pmc_ctx **out) {
     }
     // guard counters, and the lane-order self-test (lane_order_probe_kernel: 4 waves x 512 trials)
     uint32_t probe = 0;
-    if (c->guard.ensure(16) || hipMemsetAsync(c->guard.p, 0, 16, c->stream) != hipSuccess) {
+    if (c->guard.ensure(32) || hipMemsetAsync(c->guard.p, 0, 32, c->stream) != hipSuccess) {
         pmc_ctx_destroy(c);
         return PMC_E_NO_DEVICE;
     }
@@ -390,11 +391,11 @@ PMC_API int pmc_ctx_create(int device, pmc_ctx **out) {
     return PMC_OK;
 }
 
-PMC_API int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[4]) {
+PMC_API int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[5]) {
     if (!ctx || !counts) return PMC_E_ARG;
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(counts, ctx->guard.p, 16, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(counts, ctx->guard.p, 20, hipMemcpyDeviceToHost));
     return PMC_OK;
 }
 
@@ -640,10 +641,9 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     // (a context whose lane-order probe failed compresses through the single-kernel path, whose
     // sort and codes use per-lane counters and ballots instead of returning-atomic ranks)
     const bool mono = mono_env || latency || !ctx->lane_order_ok;
-    static const bool no_big = getenv("PMC_BIG_PASS") && !atoi(getenv("PMC_BIG_PASS"));
     const bool split = !force_v1 && !mono;
     const uint64_t small_lim = force_v1 ? 0 : deflate_small_limit();
-    const uint64_t big_lim = split && !no_big ? deflate_big_limit() : small_lim;
+    const uint64_t big_lim = split ? deflate_big_limit() : small_lim;
     const uint64_t v1_lim = deflate_lds_limit();
     const uint64_t lds_cut = force_v1 ? std::min<uint64_t>(v1_lim, std::max<uint64_t>(max_len, 1))
                                       : std::min<uint64_t>(small_lim, std::max<uint64_t>(max_len, 1));
@@ -701,16 +701,14 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
             if (r) return r;
         }
         static const bool no_order = getenv("PMC_TREES_ORDER") && !atoi(getenv("PMC_TREES_ORDER"));
-        // the front keeps no CRC table in LDS: its grid is sized for the blocks that really fit
-        // (PMC_FRONT_PLAN_CRC=1: the former plan, which reserved 1 KiB per block for it)
-        static const bool front_crc = getenv("PMC_FRONT_PLAN_CRC") && atoi(getenv("PMC_FRONT_PLAN_CRC"));
+        // (the front keeps no CRC table in LDS: its grid is sized for the blocks that really fit)
         const size_t tl_small = (size_t)(kTreesCap + 1) * 64 * 4 + 36 * 64 * 2;
         const size_t tl_big = (size_t)(kLCodes + 1) * 64 * 4 + 36 * 64 * 2;
         // one pass over the batch for the values with lo < len <= hi, working sets sized for pcap
         auto run_pass = [&](uint64_t lo, uint64_t hi, uint64_t pcap) -> int {
             const uint64_t fwb = deflate_front_wave_bytes(pcap), bwb = deflate_back_wave_bytes(pcap);
-            Launch Lf = plan_lds(ctx, (const void *)deflate_front_kernel, fwb, n, front_crc ? kCrcTabBytes : 0);
-            const size_t front_lds = Lf.lds - (front_crc ? kCrcTabBytes : 0);
+            Launch Lf = plan_lds(ctx, (const void *)deflate_front_kernel, fwb, n, 0);
+            const size_t front_lds = Lf.lds;
             Launch Lb = plan_lds(ctx, (const void *)deflate_back_kernel, bwb, n, kBackTabBytes);
             const uint64_t chunk = chunk_of(pcap), blocks = chunk / 64;
             uint8_t *p = (uint8_t *)ctx->split.p;
@@ -740,9 +738,8 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
             a.cap_len = pcap;
             // front work grabs: several values per grab for small values, whose parse is shorter than
             // the counter's serialised grabs (10M x 256 B: 1 per grab 114 ms, 4 or 8: 51 ms; 1 KiB: 2 per
-            // grab -0.3 %, 4 the same); PMC_FRONT_BATCH overrides
-            static const uint32_t fb_env = getenv("PMC_FRONT_BATCH") ? (uint32_t)atoi(getenv("PMC_FRONT_BATCH")) : 0u;
-            a.front_batch = fb_env ? std::min<uint32_t>(fb_env, 64u) : pcap <= 512 ? 4u : pcap <= 2048 ? 2u : 1u;
+            // grab -0.3 %, 4 the same)
+            a.front_batch = pcap <= 512 ? 4u : pcap <= 2048 ? 2u : 1u;
             for (uint64_t first = 0; first < n; first += chunk) {
                 a.first = first;
                 a.count = std::min<uint64_t>(chunk, n - first);
@@ -889,10 +886,8 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
         // members of <= kRecOutMax output bytes: the two-phase record kernel, one block per
         // resident wave (each block owns 64 record rows); larger ones: the lane kernel
         static const bool no_rec = getenv("PMC_INFLATE_REC") && !atoi(getenv("PMC_INFLATE_REC"));
-        // batches below this many members skip the record kernel (PMC_REC_MIN_N; default: none)
-        static const uint64_t rec_min_n = getenv("PMC_REC_MIN_N") ? strtoull(getenv("PMC_REC_MIN_N"), nullptr, 10) : 0;
         const unsigned lb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * 16);
-        if (!no_rec && (uint64_t)n >= rec_min_n) {
+        if (!no_rec) {
             const uint32_t rstride =
                 (uint32_t)std::min<uint64_t>(kRecMax, std::max<uint64_t>(64, ((uint64_t)max_len + 63) & ~(uint64_t)63));
             // exactly the resident blocks: a block owns its rows for the whole grid-stride loop,
@@ -935,13 +930,11 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
                                    a);
         });
         a.big_only = 0;
-        static const int diag_stop = getenv("PMC_DIAG_INFLATE_STOP") ? atoi(getenv("PMC_DIAG_INFLATE_STOP")) : 0;
-        if (diag_stop == 1) return PMC_OK; // (diagnostic: verdicts of the lane kernels, unverified)
         const unsigned vb = (unsigned)std::min<uint64_t>(((uint64_t)n + 511) / 512, (uint64_t)ctx->cus * 4);
         klaunch(ctx, PMC_K_INFLATE_VERIFY, st,
                 [&] { hipLaunchKernelGGL(inflate_verify_kernel, dim3(vb), dim3(512), 0, st, a); });
-        if (diag_stop == 2) return PMC_OK; // (diagnostic: verdicts after the CRC check)
         a.retry_only = 1;
+        a.retried = (uint32_t *)ctx->guard.p + 4; // (pmc_ctx_guard_counts counts[4])
         a.order = nullptr;
     }
     // output image capacity for the LDS kernel; the compressed input of a member whose
@@ -1097,9 +1090,7 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     const bool latency = n <= kLatencyBatch && (dir == kDecompress || max_len <= deflate_small_limit());
     // The latency path's kernel reads its inputs from, and writes its outputs to, coherent host memory in
     // place: no H2D / D2H copies (each a runtime copy kernel of its own) around its one launch.
-    // PMC_LAT_COPY=1 stages them through device memory instead (A/B).
-    static const bool lat_copy = getenv("PMC_LAT_COPY") && atoi(getenv("PMC_LAT_COPY"));
-    const bool zc = latency && !lat_copy;
+    const bool zc = latency;
     uint8_t *hp, *dp;
     int r;
     if (zc) {

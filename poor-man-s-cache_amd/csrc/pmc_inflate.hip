@@ -1143,6 +1143,7 @@ __global__ void __launch_bounds__(256, 5) inflate_kernel(InflateArgs a) {
                 }
                 continue;
             }
+            if (a.retry_only && a.retried && l == 0) atomicAdd(a.retried, 1u); // (the fast paths declined it)
             int rc;
             if (kHbm) {
                 Wh.inb = const_cast<uint8_t *>(src);

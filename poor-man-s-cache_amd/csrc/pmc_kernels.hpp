@@ -144,6 +144,7 @@ struct InflateArgs {
     uint32_t *rec_work;    // record kernel: work counter (64-member batches handed out), zeroed per launch
     uint32_t rec_max_out;  // record kernel: members of more output go to the lane kernel (<= kRecOutMax)
     int32_t multi_pass;    // lane kernel: the multi-block pass runs (mark such members kInflateMulti)
+    uint32_t *retried;     // wave kernels in retry_only mode: members they decode are counted here (or null)
 };
 
 // lane-inflate visit order: member indices grouped by compressed length, so a wave's 64

@@ -181,12 +181,12 @@ class Context:
         return {KERNEL_KINDS[k]: (ms[k], cnt[k]) for k in range(n) if cnt[k]}
 
     def guard_counts(self):
-        """Guard counters {sort, codes, probe, retry} (include/pmc_codec.h pmc_ctx_guard_counts)."""
-        c = (_u32 * 4)()
+        """Guard counters {sort, codes, probe, retry, inflate_retry} (include/pmc_codec.h pmc_ctx_guard_counts)."""
+        c = (_u32 * 5)()
         rc = lib().pmc_ctx_guard_counts(self.handle, c)
         if rc != 0:
             raise CodecUnavailable(f"pmc_ctx_guard_counts failed ({rc}): {last_error()}")
-        return {"sort": c[0], "codes": c[1], "probe": c[2], "retry": c[3]}
+        return {"sort": c[0], "codes": c[1], "probe": c[2], "retry": c[3], "inflate_retry": c[4]}
 
     def close(self):
         if self.handle:

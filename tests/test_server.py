@@ -59,8 +59,14 @@ class Server:
 
 
 def _exchange(port, cmds):
-    """One pipelined write of all commands, then read len(cmds) responses."""
+    """One pipelined write of all commands, then read len(cmds) responses.  The write waits 20 ms after the
+    connect: the reference CacheServer adds a new fd to its epoll set before it records the connection
+    (src/server/conn_manager.hpp:84-91) and reads that record without a lock (server.cpp:374, :408), so a
+    request sent at once can be lost (test_ref_server.REF_CONNECT_RACE); pmc_server has no such window,
+    and the delay costs it nothing.  A response missing for 60 s fails instead of hanging."""
     with socket.create_connection(("127.0.0.1", port)) as s:
+        s.settimeout(60)
+        time.sleep(0.02)
         s.sendall(SEP.join(cmds) + SEP)
         buf, out = b"", []
         while len(out) < len(cmds):
