@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--h2h-chunk", type=int, default=0, help="values per chunk of the pipelined h2h leg (0 = n/16)")
     ap.add_argument("--mix", action="store_true",
                     help="BASELINE configs[2]: SET/GET mix over a device-resident compressed store instead")
+    ap.add_argument("--batches", action="store_true",
+                    help="server-shaped batches (256 / 1,024 / 4,096 / 400 values, default 4 KiB): ms per batch")
     ap.add_argument("--mix-keys", type=int, default=1_000_000)
     ap.add_argument("--mix-serial", action="store_true", help="SETs and GETs of a batch on one stream")
     ap.add_argument("--mix-ops", type=int, default=1_048_576)
@@ -335,8 +337,97 @@ def mix_bench(args):
     ctx.close()
 
 
+def batch_bench(args):
+    """Server-shaped batches (BASELINE configs[4]): what one epoll iteration of a
+    batched server hands the codec.  Batches of 256 / 1,024 / 4,096 JSON-slice values (default 4 KiB), timed
+    per batch: device-resident (pmc_gzip_*_batch, HIP events around each call on its stream) and host-resident
+    (pmc_gzip_*_batch_host: pinned staging, H2D, kernels, D2H, host wall clock), compress and decompress
+    separately, every member checked against the value it came from."""
+    import numpy as np
+    import torch
+
+    import pmc_codec
+    from pmc_codec import device as D
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    L = pmc_codec.lib()
+    ctx = pmc_codec.Context(0)
+    sh = torch.cuda.current_stream().cuda_stream
+    corpus_b = load_corpus()
+    vlen, reps = args.vlen, 20
+    out = []
+    corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).to(dev)
+    for n in (256, 1024, 4096, 400):
+        raw = torch.empty(n * vlen + 16, dtype=torch.uint8, device=dev)
+        assert L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), 0x5EED, 0, 0, None, n, vlen, raw.data_ptr(), sh) == 0
+        rh = raw.cpu().numpy().tobytes()
+        vals = [rh[i * vlen:(i + 1) * vlen] for i in range(n)]
+        b = D.pack(vals, dev)
+        D.compress(ctx, b)  # (untimed: sizes the scratch)
+        torch.cuda.synchronize()
+        # (each call timed by events around it on the stream; output slots allocated outside)
+        tc = []
+        for r in range(reps):
+            caps = [pmc_codec.gzip_bound(vlen)] * n
+            dst, doff, dcap = D.slots_for(caps, dev)
+            dlen = torch.zeros(n, dtype=torch.int32, device=dev)
+            rcc = torch.zeros(n, dtype=torch.int32, device=dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ctx.compress_device(b.data, b.off, b.len, dst, doff, dcap, dlen, rcc, vlen, sh)
+            e1.record()
+            torch.cuda.synchronize()
+            tc.append(e0.elapsed_time(e1))
+        comp = D.Batch(dst, doff, dlen, n, int(max(caps)))
+        assert int((rcc != 0).sum()) == 0
+        members = comp.host_items()
+        D.decompress(ctx, comp, [vlen] * n)
+        torch.cuda.synchronize()
+        td = []
+        for r in range(reps):
+            back_dst, boff, bcap = D.slots_for([vlen] * n, dev)
+            blen = torch.zeros(n, dtype=torch.int32, device=dev)
+            brc = torch.zeros(n, dtype=torch.int32, device=dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ctx.decompress_device(comp.data, comp.off, comp.len, back_dst, boff, bcap, blen, brc, vlen, sh)
+            e1.record()
+            torch.cuda.synchronize()
+            td.append(e0.elapsed_time(e1))
+        back = D.Batch(back_dst, boff, blen, n, vlen).host_items()
+        bad = int((brc != 0).sum()) + sum(1 for v, w in zip(vals, back) if v != w)
+        # host-resident batches (what the server hook calls), wall clock
+        hc, hd = [], []
+        for r in range(reps):
+            t0 = time.perf_counter()
+            res = ctx.compress_many(vals)
+            hc.append((time.perf_counter() - t0) * 1e3)
+        hm = [g for _, g in res]
+        bad += sum(1 for (r_, g), m in zip(res, members) if r_ != 0 or g != m)
+        for r in range(reps):
+            t0 = time.perf_counter()
+            resd = ctx.decompress_many(hm, [vlen] * n)
+            hd.append((time.perf_counter() - t0) * 1e3)
+        bad += sum(1 for (r_, v2), v in zip(resd, vals) if r_ != 0 or v2 != v)
+        med = lambda x: float(np.median(x))
+        out.append({"values": n, "value_bytes": vlen,
+                    "device_ms": {"compress": med(tc), "decompress": med(td)},
+                    "host_ms": {"compress": med(hc), "decompress": med(hd)},
+                    "mismatches": bad})
+        print(json.dumps(out[-1]), file=sys.stderr, flush=True)
+    print(json.dumps({"metric": "server-shaped batch latency (ms per batch, median of 20)", "unit": "ms",
+                      "higher_is_better": False, "dtype": "u8", "data": "synthetic: JSON slices of the "
+                      "reference's tests/data corpus (seed 0x5EED)", "batches": out}), flush=True)
+    ctx.close()
+
+
 def main():
     args = parse()
+    if args.batches:
+        if args.vlen == 1024:
+            args.vlen = 4096
+        return batch_bench(args)
     if args.mix:
         if args.vlen == 1024:
             args.vlen = 4096

@@ -106,6 +106,33 @@ bool exchange(int fd, const std::string &req, std::string &buf, size_t n, std::v
     return sent == req.size();
 }
 
+// Until the server answers a throwaway GET (up to 60 s): the reference CacheServer listens ~2 s before
+// it accepts (its constructor sieves primes for every shard), and a request waiting in the backlog is
+// read the moment its fd joins the epoll set, inside the connect race of
+// /root/reference/src/server/conn_manager.hpp:84-91 (epoll registration before the ConnectionData is
+// recorded) and server.cpp:374,408 (that map read without its lock), where it may never be answered.
+bool warm_up(int port) {
+    const auto t0 = std::chrono::steady_clock::now();
+    std::string buf;
+    std::vector<std::string> out;
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60)) {
+        const int fd = connect_to(port);
+        if (fd >= 0) {
+            pollfd pf{fd, POLLOUT, 0};
+            const std::string req = "GET __warmup__\x1f";
+            bool ok = send(fd, req.data(), req.size(), MSG_NOSIGNAL) == (ssize_t)req.size();
+            pf.events = POLLIN;
+            ok = ok && poll(&pf, 1, 1000) > 0 && (pf.revents & POLLIN);
+            char tmp[256];
+            ok = ok && recv(fd, tmp, sizeof tmp, 0) > 0;
+            close(fd);
+            if (ok) return true;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+    return false;
+}
+
 struct Worker {
     uint64_t ops = 0, sets = 0, gets = 0, bytes = 0, bad = 0;
 };
@@ -160,6 +187,8 @@ int main(int argc, char **argv) {
                     failed++;
                     return;
                 }
+                // (the first write 20 ms after the connect, past the reference server's registration window)
+                std::this_thread::sleep_for(std::chrono::milliseconds(20));
                 std::vector<uint64_t> mine;
                 for (uint64_t k = c; k < o.keys; k += o.conns) mine.push_back(k);
                 std::vector<uint64_t> ver(mine.size(), 0);
@@ -212,6 +241,10 @@ int main(int argc, char **argv) {
             });
         for (auto &t : th) t.join();
     };
+    if (!warm_up(o.port)) {
+        fprintf(stderr, "server on port %d did not answer within 60 s\n", o.port);
+        return 1;
+    }
     run_phase(true);
     for (auto &x : w) x = Worker{};
     const auto t0 = std::chrono::steady_clock::now();

@@ -16,3 +16,9 @@ for cfg in "40000 65536" "1000 1048576" "100000 30000"; do
   timeout -k 10 300 python bench.py --no-cpu-baseline --n $1 --vlen $2 --steps 2 > gpurun_out/$T/b_$2.json 2> gpurun_out/$T/b_$2.err || exit $?
   python3 -c "import json;d=json.load(open('gpurun_out/$T/b_$2.json'));print('$2',d['value'],d['compress_gib_s'],d['decompress_gib_s'],d['mismatches'],d['roofline']['kernel_ms_per_step'])"
 done
+# server-shaped batches: the default routing, then the wave-per-member inflate for comparison
+timeout -k 10 300 python bench.py --batches > gpurun_out/$T/batches.json 2> gpurun_out/$T/batches.err || exit $?
+PMC_INFLATE_WAVE=1 timeout -k 10 300 python bench.py --batches > gpurun_out/$T/batches_wave.json 2> gpurun_out/$T/batches_wave.err || exit $?
+cat gpurun_out/$T/batches.err gpurun_out/$T/batches_wave.err
+OUT=gpurun_out/$T/refsrv timeout -k 10 600 bash scripts/ref_server_bench.sh > gpurun_out/$T/refsrv.log 2>&1; rc=$?
+tail -12 gpurun_out/$T/refsrv.log; exit $rc
