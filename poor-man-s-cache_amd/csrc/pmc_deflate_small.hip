@@ -119,12 +119,21 @@ struct FrontLayout {
     int pkb;             // chain-count bits packed into R's top (front_pkb), 0: CN array, -1: HC only
     uint64_t cn, hc, ev; // parse scratch in X (cn unused when pk); the sort's 512-B table at X
 };
+// PMC_FRONT_S10: at values of <= 1 KiB (pkb 6) the sorted positions (< 1024, 10 bits) are packed three
+// to a word, which takes the front's LDS from 5,696 to 5,008 B per wave: 32 resident waves per CU (8 per
+// SIMD) instead of 28, with the kernel held to 64 VGPRs (pmc_deflate_split.hip).  The region keeps at
+// least 256 B: the sort parks its 128 high-digit counters there (sort_positions2_body).
+#ifndef PMC_FRONT_S10
+#define PMC_FRONT_S10 0
+#endif
+__host__ __device__ inline bool front_s10(uint64_t n) { return PMC_FRONT_S10 && front_pkb(n) == 6; }
 __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
     auto a = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
     FrontLayout F;
     F.bytes = 0;
     F.S = a(n + 32);
-    F.R = F.S + a(2 * n + 2);
+    const uint64_t s_bytes = front_s10(n) ? (((n + 2) / 3) * 4 > 256 ? ((n + 2) / 3) * 4 : 256) : 2 * n + 2;
+    F.R = F.S + a(s_bytes);
     F.X = F.R + a(2 * n + 2);
     F.pkb = front_pkb(n);
     F.cn = F.X;
@@ -305,6 +314,7 @@ struct SmallWave {
     PMC_LDS uint8_t *b;
     PMC_LDS uint32_t *bw;
     PMC_LDS uint16_t *S, *R;
+    uint32_t s10 = 0; // front at <= 1 KiB (front_s10): S packed three 10-bit positions per word (sget)
     PMC_LDS uint32_t *lfreq, *dfreq, *blfreq;
     PMC_LDS uint32_t *outw;
     PMC_LDS uint8_t *outb;
@@ -350,6 +360,16 @@ struct SmallWave {
 #define PMC_STOP(k, ret)
 #endif
 
+    // sorted position k: packed (PK 6 with PMC_FRONT_S10: entry k is bits 10 (k % 3) .. of word k / 3) or u16
+    template <int PK>
+    __device__ __forceinline__ uint32_t sget(uint32_t k) const {
+        if constexpr (PK == 6 && PMC_FRONT_S10) {
+            const uint32_t w = __umul24(k, 0xAAABu) >> 17; // k / 3 for k < 98304
+            return (((PMC_LDS const uint32_t *)S)[w] >> (10 * (k - 3 * w))) & 1023u;
+        } else {
+            return S[k];
+        }
+    }
     __device__ uint32_t load4(uint32_t p) const {
         uint32_t w0 = bw[p >> 2], w1 = bw[(p >> 2) + 1];
         return __builtin_amdgcn_alignbyte(w1, w0, p & 3);
@@ -459,6 +479,7 @@ struct SmallWave {
             hiw[l] = c0 | (c0 + u0) << 16;
             wave_sync();
         }
+        const uint32_t pk10 = s10; // (packed S: the second scatter ORs 10-bit fields into zeroed words)
         for (int pass = 0; pass < 2; pass++) {
             const uint32_t sh = pass ? 8 : 0;
             PMC_LDS uint16_t *dst = pass ? S : Tt;
@@ -480,6 +501,10 @@ struct SmallWave {
                 scan_tab();
                 wave_sync();
             }
+            if (pass && pk10) {
+                for (uint32_t k = l; k < (npos + 2) / 3; k += 64) ((PMC_LDS uint32_t *)S)[k] = 0u;
+                wave_sync();
+            }
             // a lane's slot from one returning LDS atomic on its digit's counter: the lanes of one
             // ds_add_rtn to a word get their old values in lane order (scripts/micro/
             // lds_atomic_order.hip: 16.7M trials of skewed digit mixes, none out of order), so the
@@ -492,7 +517,15 @@ struct SmallWave {
 #endif
                 const uint32_t p = x < npos ? (pass ? (uint32_t)Tt[x] : x) : 0u;
                 const uint32_t d = (hash3(load4(p)) >> sh) & 255, hs = 16 * (d & 1);
-                if (x < npos) dst[(lds_add(&tab[d >> 1], 1u << hs) >> hs) & 0xffffu] = (uint16_t)p;
+                if (x < npos) {
+                    const uint32_t slot = (lds_add(&tab[d >> 1], 1u << hs) >> hs) & 0xffffu;
+                    if (pass && pk10) {
+                        const uint32_t w = __umul24(slot, 0xAAABu) >> 17;
+                        lds_or((PMC_LDS uint32_t *)S + w, p << (10 * (slot - 3 * w)));
+                    } else {
+                        dst[slot] = (uint16_t)p;
+                    }
+                }
             }
             wave_sync();
         }
@@ -626,7 +659,7 @@ struct SmallWave {
             const uint32_t wthr = thr >= 4 ? load4(i + thr - 3) : 0u;
             const int k = kb - l;
             const uint32_t ord = examined + (uint32_t)l;
-            uint32_t q = k >= 0 ? S[k] : 0u;
+            uint32_t q = k >= 0 ? sget<PK>((uint32_t)k) : 0u;
             uint32_t wq = load4(q);
             // position 0 is zlib's NIL (head[] value 0): never a match source; it is the
             // lowest position of its hash run, so valid lanes stay a prefix
@@ -806,7 +839,7 @@ struct SmallWave {
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
             const uint32_t k = c0 + l;
             const bool valid = k < npos;
-            const uint32_t p = valid ? (uint32_t)S[k] : 0u;
+            const uint32_t p = valid ? sget<PK>(k) : 0u;
             const uint32_t h = valid ? hash3(load4(p)) : 0xfffffffeu;
             uint32_t hp = (uint32_t)__shfl_up((int)h, 1), pp = (uint32_t)__shfl_up((int)p, 1);
             hp = l == 0 ? ph : hp;
@@ -907,7 +940,7 @@ struct SmallWave {
         const uint32_t own = v ? ((sc >> 19) & 127) - 1 : 0u;
         const uint32_t P = p0 + own, d = l - (sc >> 26) + 1;
         const uint32_t rxo = sc & 0x7ffffu;
-        uint32_t q = S[v && (!SAT || rxo >= d) ? rxo - d : 0u];
+        uint32_t q = sget<PK>(v && (!SAT || rxo >= d) ? rxo - d : 0u);
         uint64_t A0, A1, B0, B1;
         load16(P, A0, A1);
         q = v ? q : 0u;

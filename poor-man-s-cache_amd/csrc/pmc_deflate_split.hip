@@ -28,7 +28,8 @@ namespace pmc {
 // interleaved by 64-value block (lane-coalesced).
 
 // ---- front -------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
+// (8 waves per SIMD with PMC_FRONT_S10: the packed S leaves room for them at <= 1 KiB; 7 otherwise)
+__global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
     uint8_t *base = lds + (uint64_t)wib * a.wave_bytes;
@@ -42,6 +43,7 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     w.HC = to_lds<uint64_t>(base + F.hc);
     w.EV = to_lds<uint32_t>(base + F.ev);
     w.cnp = F.pkb;
+    w.s10 = front_s10(a.cap_len) ? 1u : 0u;
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;

@@ -6,6 +6,9 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <unordered_map>
 
 #include "gzip_compressor.hpp"
@@ -194,38 +197,89 @@ uint64_t fingerprint(const char *p, size_t n) {
 
 } // namespace
 
+// One compress batch: its arrays (built on the request thread) and its results; run() touches nothing
+// else, so it may run on a helper thread (PrimeCompressAsync) while the request thread does the GETs.
+struct CompressJob {
+    std::vector<uint64_t> src_off, dst_off;
+    std::vector<uint32_t> src_len, dst_cap, dst_len;
+    std::vector<int32_t> rc;
+    std::vector<uint8_t> dst;
+    const char *vals = nullptr;
+    int r = PMC_OK;
+    bool build(PrimeState &P, const std::vector<std::string_view> &values) {
+        uint64_t dof = 0;
+        for (const auto &v : values) {
+            if (v.size() + 1 < kMinCompressSize || v.size() > 0xffffffffull) continue;  // kvs.cpp:182
+            src_off.push_back(P.cvals.size());
+            src_len.push_back((uint32_t)v.size());
+            P.cvals.append(v.data(), v.size());
+            dst_off.push_back(dof);
+            dst_cap.push_back((uint32_t)pmc_gzip_bound(v.size()));
+            dof += dst_cap.back();
+        }
+        vals = P.cvals.data();  // (stable: nothing appends to cvals until finish())
+        dst.resize(dof + 1);
+        dst_len.resize(src_len.size());
+        rc.assign(src_len.size(), 0);
+        return !src_len.empty();
+    }
+    void run(pmc_ctx *ctx) {
+        r = ctx ? pmc_gzip_compress_batch_host(ctx, (const uint8_t *)vals, src_off.data(), src_len.data(),
+                                               (uint32_t)src_len.size(), dst.data(), dst_off.data(), dst_cap.data(),
+                                               dst_len.data(), rc.data())
+                : PMC_E_NO_DEVICE;
+    }
+    void finish(PrimeState &P) {
+        P.stats.batches++;
+        for (size_t k = 0; k < src_len.size(); k++) {
+            if (r || rc[k] != OPERATION_SUCCESS) continue;  // not primed: Compress runs (and fails) itself
+            char *d = new char[dst_len[k]];
+            memcpy(d, dst.data() + dst_off[k], dst_len[k]);
+            const uint32_t idx = (uint32_t)P.comp.size();
+            P.comp.push_back({src_off[k], src_len[k], d, dst_len[k], {}});
+            P.cidx.emplace(fingerprint(P.cvals.data() + src_off[k], src_len[k]), idx);
+        }
+    }
+};
+
 void PrimeCompress(const std::vector<std::string_view> &values, pmc_ctx *ctx) {
     PrimeState &P = g_prime;
-    std::vector<uint64_t> src_off, dst_off;
-    std::vector<uint32_t> src_len, dst_cap;
-    uint64_t dof = 0;
-    for (const auto &v : values) {
-        if (v.size() + 1 < kMinCompressSize || v.size() > 0xffffffffull) continue;  // kvs.cpp:182
-        src_off.push_back(P.cvals.size());
-        src_len.push_back((uint32_t)v.size());
-        P.cvals.append(v.data(), v.size());
-        dst_off.push_back(dof);
-        dst_cap.push_back((uint32_t)pmc_gzip_bound(v.size()));
-        dof += dst_cap.back();
-    }
-    const uint32_t m = (uint32_t)src_len.size();
-    if (!m) return;
-    if (!ctx) ctx = pmc_default_ctx();
-    std::vector<uint8_t> dst(dof + 1);
-    std::vector<uint32_t> dst_len(m);
-    std::vector<int32_t> rc(m, 0);
-    const int r = ctx ? pmc_gzip_compress_batch_host(ctx, (const uint8_t *)P.cvals.data(), src_off.data(), src_len.data(),
-                                                     m, dst.data(), dst_off.data(), dst_cap.data(), dst_len.data(),
-                                                     rc.data())
-                      : PMC_E_NO_DEVICE;
-    P.stats.batches++;
-    for (uint32_t k = 0; k < m; k++) {
-        if (r || rc[k] != OPERATION_SUCCESS) continue;  // not primed: Compress runs (and fails) itself
-        char *d = new char[dst_len[k]];
-        memcpy(d, dst.data() + dst_off[k], dst_len[k]);
-        const uint32_t idx = (uint32_t)P.comp.size();
-        P.comp.push_back({src_off[k], src_len[k], d, dst_len[k], {}});
-        P.cidx.emplace(fingerprint(P.cvals.data() + src_off[k], src_len[k]), idx);
+    CompressJob job;
+    if (!job.build(P, values)) return;
+    job.run(ctx ? ctx : pmc_default_ctx());
+    job.finish(P);
+}
+
+namespace {
+// PrimeCompressAsync's job and helper thread (per request thread)
+thread_local std::unique_ptr<CompressJob> g_job;
+thread_local std::thread g_job_thread;
+// A context of its own: host calls of one context run one at a time (pmc_codec.h), and this one runs
+// beside the default context's decompress batch, on its own stream.
+pmc_ctx *compress_ctx() {
+    static std::once_flag once;
+    static pmc_ctx *c = nullptr;
+    std::call_once(once, [] {
+        if (pmc_ctx_create(0, &c) != PMC_OK) c = nullptr;
+    });
+    return c ? c : pmc_default_ctx();
+}
+} // namespace
+
+void PrimeCompressAsync(const std::vector<std::string_view> &values) {
+    PrimeCompressWait();
+    auto job = std::make_unique<CompressJob>();
+    if (!job->build(g_prime, values)) return;
+    CompressJob *j = job.get();
+    g_job = std::move(job);
+    g_job_thread = std::thread([j] { j->run(compress_ctx()); });
+}
+
+void PrimeCompressWait() {
+    if (g_job_thread.joinable()) g_job_thread.join();
+    if (g_job) {
+        g_job->finish(g_prime);
+        g_job.reset();
     }
 }
 

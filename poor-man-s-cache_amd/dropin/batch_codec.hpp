@@ -64,6 +64,12 @@ std::vector<char *> DecompressForGet(const std::vector<Entry> &entries, std::vec
 /// values shorter than kMinCompressSize - 1 are skipped).  A later Compress(v) with the same bytes
 /// gets the primed member (matched by content: kvs copies the value before compressing it).
 void PrimeCompress(const std::vector<std::string_view> &values, pmc_ctx *ctx = nullptr);
+/// PrimeCompress with the device batch on a helper thread and a context of its own, so the iteration's
+/// GET dry run and decompress batch (BeginCollect .. PrimeCollected, on the default context) overlap it;
+/// PrimeCompressWait() joins it and files its results (call it before the values are compressed).
+/// The views must stay valid until then.
+void PrimeCompressAsync(const std::vector<std::string_view> &values);
+void PrimeCompressWait();
 
 /// Between BeginCollect() and PrimeCollected(), Decompress(ptr, size) only records (ptr, size) and
 /// returns {nullptr, INVALID_INPUT}: a dry run of the batch's GETs (kvs::get is a pure lookup)

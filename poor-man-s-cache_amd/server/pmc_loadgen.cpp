@@ -42,7 +42,7 @@ uint64_t splitmix64(uint64_t x) {
 }
 
 struct Opts {
-    int port = 9001, conns = 16, batch = 100, mix = 50;
+    int port = 9001, conns = 16, batch = 100, mix = 50, warmup_sec = 60;
     uint64_t keys = 65536, vlen = 4096, ops = 200000;
     std::string data;
 };
@@ -106,16 +106,19 @@ bool exchange(int fd, const std::string &req, std::string &buf, size_t n, std::v
     return sent == req.size();
 }
 
-// Until the server answers a throwaway GET (up to 60 s): the reference CacheServer listens ~2 s before
+// Until the server answers a throwaway GET (up to `secs`): the reference CacheServer listens ~2 s before
 // it accepts (its constructor sieves primes for every shard), and a request waiting in the backlog is
 // read the moment its fd joins the epoll set, inside the connect race of
-// /root/reference/src/server/conn_manager.hpp:84-91 (epoll registration before the ConnectionData is
-// recorded) and server.cpp:374,408 (that map read without its lock), where it may never be answered.
-bool warm_up(int port) {
+// /root/reference/src/server/conn_manager.hpp:83-93 (epoll registration before the ConnectionData is
+// recorded) and server.cpp:373,409 (that map read without its lock), where it may never be answered.
+// A reference server whose accept thread has self-deadlocked (validateConnections holds conn_mutex and
+// calls closeConnection, which locks it again: conn_manager.hpp:109, :117, :142) never answers; the
+// caller restarts it (scripts/ref_server_bench.sh), so a short --warmup-sec keeps that cheap.
+bool warm_up(int port, int secs) {
     const auto t0 = std::chrono::steady_clock::now();
     std::string buf;
     std::vector<std::string> out;
-    while (std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60)) {
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::seconds(secs)) {
         const int fd = connect_to(port);
         if (fd >= 0) {
             pollfd pf{fd, POLLOUT, 0};
@@ -151,6 +154,7 @@ int main(int argc, char **argv) {
         else if (a == "--ops") o.ops = strtoull(v.c_str(), nullptr, 10);
         else if (a == "--mix") o.mix = atoi(v.c_str());
         else if (a == "--data") o.data = v;
+        else if (a == "--warmup-sec") o.warmup_sec = atoi(v.c_str());
         else {
             fprintf(stderr, "unknown option %s\n", a.c_str());
             return 2;
@@ -241,8 +245,8 @@ int main(int argc, char **argv) {
             });
         for (auto &t : th) t.join();
     };
-    if (!warm_up(o.port)) {
-        fprintf(stderr, "server on port %d did not answer within 60 s\n", o.port);
+    if (!warm_up(o.port, o.warmup_sec)) {
+        fprintf(stderr, "server on port %d did not answer within %d s\n", o.port, o.warmup_sec);
         return 1;
     }
     run_phase(true);

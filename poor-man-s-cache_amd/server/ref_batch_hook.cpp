@@ -8,7 +8,8 @@
 // requests exactly as before, and calls endCodecBatch() after the responses went out.
 //
 // primeCodecBatch() makes the iteration's codec work two device batch calls instead of one
-// GzipCompressor call per value (kvs.cpp:183, :233):
+// GzipCompressor call per value (kvs.cpp:183, :233), the compress batch on a helper thread and context of
+// its own so that it overlaps the GET side:
 //   * SET: every value the iteration will store (custom protocol "SET key value", RESP
 //     "*3 $3 SET ..."), as the C string kvs::insertEntry will hand to Compress (strlen semantics,
 //     kvs.cpp:148), is compressed by pmc_batch::PrimeCompress in one call;
@@ -119,7 +120,9 @@ void CacheServer::primeCodecBatch(const std::vector<int> &fds) {
             }
         }
     }
-    if (!set_values.empty()) pmc_batch::PrimeCompress(set_values);
+    // the SET batch runs on a helper thread (its own context and stream) while this thread does the GET
+    // dry run and the decompress batch: the two device batches overlap
+    if (!set_values.empty()) pmc_batch::PrimeCompressAsync(set_values);
     if (!get_keys.empty()) {
         pmc_batch::BeginCollect();
         for (const std::string &k : get_keys) {
@@ -128,6 +131,7 @@ void CacheServer::primeCodecBatch(const std::vector<int> &fds) {
         }
         pmc_batch::PrimeCollected();
     }
+    pmc_batch::PrimeCompressWait();
 }
 
 namespace {

@@ -19,6 +19,7 @@ done
 # server-shaped batches: the default routing, then the wave-per-member inflate for comparison
 timeout -k 10 300 python bench.py --batches > gpurun_out/$T/batches.json 2> gpurun_out/$T/batches.err || exit $?
 PMC_INFLATE_WAVE=1 timeout -k 10 300 python bench.py --batches > gpurun_out/$T/batches_wave.json 2> gpurun_out/$T/batches_wave.err || exit $?
-cat gpurun_out/$T/batches.err gpurun_out/$T/batches_wave.err
+PMC_DEFLATE_MONO=1 timeout -k 10 300 python bench.py --batches > gpurun_out/$T/batches_mono.json 2> gpurun_out/$T/batches_mono.err || exit $?
+cat gpurun_out/$T/batches.err gpurun_out/$T/batches_wave.err gpurun_out/$T/batches_mono.err
 OUT=gpurun_out/$T/refsrv timeout -k 10 600 bash scripts/ref_server_bench.sh > gpurun_out/$T/refsrv.log 2>&1; rc=$?
 tail -12 gpurun_out/$T/refsrv.log; exit $rc

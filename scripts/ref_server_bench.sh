@@ -6,10 +6,11 @@
 #           (server.cpp:631-643) -- the CPU baseline of this config, timed on this host
 #   dropin  the drop-in GzipCompressor, one GPU call per value
 #   batch   the drop-in + the f1 batch hook (one device batch per direction per epoll iteration)
-# pmc_loadgen waits until a server answers and writes 20 ms after connecting, which keeps clear of the
-# reference's connect race (conn_manager.hpp:84-91, server.cpp:374,408); a server
-# that still never answers (the race can corrupt its connection map at start-up) is restarted, at most
-# three times per case.
+# No connection before a server prints its ready line; pmc_loadgen then waits (10 s) until it answers
+# and writes 20 ms after connecting, which keeps clear of the reference's connect race (INTEGRATION.md
+# 3.2.1: conn_manager.hpp:83-93, server.cpp:373,409).  A reference server that never answers has
+# self-deadlocked (validateConnections -> closeConnection relocks conn_mutex, conn_manager.hpp:117, :142;
+# about half of all starts on a long-running host): it is killed and started again, at most five times.
 #   OUT=gpurun_out/x bash scripts/ref_server_bench.sh
 cd "$GRAFT_REPO_ROOT" || cd "$(dirname "$0")/.." || exit 1
 OUT=${OUT:-gpurun_out/refsrv}
@@ -20,8 +21,11 @@ once() {  # tag cmd... : start a server (cmd), run the load, stop it
     local port=$((20000 + RANDOM % 20000))
     "$@" $port > "$OUT/server_$tag.log" 2>&1 &
     local pid=$!
+    # no connection before the server's Start() prints its ready line (connections queued in the backlog
+    # meanwhile are accepted together, inside the reference's connect race)
+    for k in $(seq 1 600); do grep -q "ready to accept\|READY" "$OUT/server_$tag.log" 2>/dev/null && break; sleep 0.1; done
     timeout -k 5 240 $B/pmc_loadgen --port $port --data tests/golden/data --vlen $VLEN --ops $OPS --conns $CONNS \
-        --keys $KEYS --batch 100 --mix 50 > "$OUT/load_$tag.json" 2> "$OUT/load_$tag.err"
+        --keys $KEYS --batch 100 --mix 50 --warmup-sec 10 > "$OUT/load_$tag.json" 2> "$OUT/load_$tag.err"
     local rc=$?
     kill $pid; sleep 2; kill -9 $pid 2>/dev/null; wait $pid 2>/dev/null
     return $rc
@@ -30,14 +34,14 @@ ref_server() { SERVER_PORT=$2 NUM_SHARDS=128 PMC_PRIME_STATS="$OUT/prime_$1_${VL
 pmc_srv() { $B/pmc_server --port $2 --codec $1 --heap-mb 8192; }
 case_() {  # label server-fn kind
     local tag="$1_${VLEN}_${CONNS}_${KEYS}"
-    for attempt in 1 2 3; do
+    for attempt in 1 2 3 4 5; do
         if once "$tag" $2 $3; then
             sed "s/^{/{\"server\": \"$1\", \"attempt\": $attempt, /" "$OUT/load_$tag.json" | tee -a "$OUT/ref_server_bench.jsonl"
             return 0
         fi
         grep -q "did not answer" "$OUT/load_$tag.err" || { cat "$OUT/load_$tag.err"; return 1; }
     done
-    echo "{\"server\": \"$1\", \"failed\": \"no answer after 3 starts\", \"vlen\": $VLEN, \"conns\": $CONNS}" | tee -a "$OUT/ref_server_bench.jsonl"
+    echo "{\"server\": \"$1\", \"failed\": \"no answer after 5 starts\", \"vlen\": $VLEN, \"conns\": $CONNS}" | tee -a "$OUT/ref_server_bench.jsonl"
 }
 for shape in "4096 16 8192 40000" "4096 64 65536 100000" "1024 16 8192 40000"; do
     set -- $shape

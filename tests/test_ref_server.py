@@ -41,24 +41,48 @@ class RefServer:
         if tmp_path is not None:
             self.stats = str(tmp_path / f"prime_{kind}.json")
             env["PMC_PRIME_STATS"] = self.stats
-        self.p = subprocess.Popen([exe], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         # Up means answering, not only listening: the CacheServer listens from its constructor, but accepts
         # only once Start() runs, ~2 s later (the Primegen sieve of every shard's KeyValueStore runs
-        # between).  A request that waits in the backlog meanwhile is read the moment its fd joins the epoll
-        # set -- inside REF_CONNECT_RACE's window -- and is often never answered; so a throwaway GET is
-        # retried on fresh connections until one is answered.
+        # between).  Connections that wait in the backlog meanwhile are accepted together the moment the
+        # accept thread starts, all inside REF_CONNECT_RACE's window.  So no connection is made before
+        # Start() has printed its ready line (server.cpp:645, flushed by std::endl); then a throwaway GET
+        # is retried on fresh connections until answered.  A start whose first connection hits
+        # REF_SELF_DEADLOCK never answers anything: it is killed and the server started again, up to five
+        # times (about half of all starts deadlock on this host); five dead starts xfail with the citation.
+        self.exe, self.env, self.starts = exe, env, []
+        for attempt in range(5):
+            if self._start():
+                return
+        pytest.xfail(f"{REF_SELF_DEADLOCK}; {len(self.starts)} starts: {self.starts}")
+
+    def _start(self):
+        import select
+        self.port = _free_port()  # (a fresh port per start: the killed one's may linger in TIME_WAIT)
+        self.env["SERVER_PORT"] = str(self.port)
+        self.p = subprocess.Popen([self.exe], env=self.env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
         t0 = time.time()
-        while True:
+        seen = ""
+        while "ready to accept connections" not in seen:
             assert self.p.poll() is None, self.p.stderr.read()
-            assert time.time() - t0 < 60, "server did not come up"
+            assert time.time() - t0 < 60, "server did not start: " + seen[-500:]
+            if select.select([self.p.stdout], [], [], 0.5)[0]:  # (raw reads: select sees the fd, not Python's buffer)
+                seen += os.read(self.p.stdout.fileno(), 4096).decode(errors="replace")
+        t1 = time.time()
+        while time.time() - t1 < 10:
+            assert self.p.poll() is None, self.p.stderr.read()
             try:
                 with socket.create_connection(("127.0.0.1", self.port), timeout=1) as c:
                     c.settimeout(1)
                     c.sendall(b"GET __warmup__\x1f")
                     if c.recv(64):
-                        break
+                        self.starts.append("answered")
+                        return True
             except OSError:
                 time.sleep(0.05)
+        self.starts.append("deadlocked" if _deadlocked(self.p.pid) else "silent")
+        self.p.kill()
+        self.p.communicate()
+        return False
 
     def stop(self, timeout=30):
         self.p.send_signal(signal.SIGTERM)  # this exact child: main's handler calls CacheServer::Stop
@@ -80,19 +104,43 @@ class RefServer:
         return None
 
 
-# A defect of the reference server itself, whatever the codec under kvs: its accept thread adds a new
-# client fd to the epoll set (src/server/conn_manager.hpp:84-87, EPOLLIN | EPOLLET) before it inserts the
-# fd's ConnectionData into ConnManager::connections (:91), and the request thread reaches that
-# std::unordered_map with operator[] and no lock (src/server/server.cpp:408 in readRequestAsync, :374 in
-# handleRequests) while the accept thread inserts (:91) and erases (validateConnections -> closeConnection,
-# :108-121, :131-157) under conn_mutex.  A client that writes right after connecting -- the harness's
-# workers do -- races the two threads on the map: the first pipelined batch is read into a node the map
-# does not keep, so its requests are never answered (the harness then waits on readuntil forever) or a
-# command split between two nodes' buffers is answered "ERROR: Unknown command" (seen on
-# ref_server_zlib, the reference exactly as deployed: 5 failed and 1 hung run of 12 here, always at the
-# first batch of a connection).
-REF_CONNECT_RACE = ("reference defect: conn_manager.hpp:84-91 registers the fd with epoll before inserting "
-                    "its ConnectionData, server.cpp:374/:408 read the connections map without conn_mutex")
+# Two defects of the reference server itself, whatever the codec under kvs.
+#
+# REF_CONNECT_RACE: its accept thread adds a new client fd to the epoll set (src/server/conn_manager.hpp:
+# 83-86, EPOLLIN | EPOLLET) before it inserts the fd's ConnectionData into ConnManager::connections
+# (:91-93), and the request thread reaches that std::unordered_map with operator[] and no lock
+# (src/server/server.cpp:409 in readRequestAsync, :373 in handleRequests) while the accept thread inserts
+# (:93) and erases (closeConnection, :141-169) under conn_mutex.  A client that writes right after
+# connecting -- the harness's workers do -- races the two threads on the map: the first pipelined batch is
+# read into a node the map does not keep, so its requests are never answered or a command split between
+# two nodes' buffers is answered "ERROR: Unknown command" (seen on ref_server_zlib, the reference exactly as
+# deployed: 5 failed and 1 hung run of 12 here, always at the first batch of a connection).
+#
+# REF_SELF_DEADLOCK: validateConnections (conn_manager.hpp:108-123, run by the accept thread on every idle
+# accept() while any connection is counted, :181-182) holds conn_mutex (:109) and calls closeConnection
+# (:117) for any entry idle longer than MAX_CONN_LIFETIME_SEC (300 s, constants.hpp:36); closeConnection
+# locks the same non-recursive std::mutex again (:142), so the accept thread blocks forever and the request
+# thread follows at its next updateActivity (:130, from server.cpp:355): the server never answers again.
+# A ConnectionData made by default construction carries lastActivity {0, 0} (:58), so the entry looks idle
+# for the host's whole CLOCK_MONOTONIC uptime.  Taken from a -O0 -g build of the same sources in a hung
+# state (/proc/<pid>/task/*/syscall: both threads in futex; their stacks read through /proc/<pid>/mem and
+# addr2line): accept thread acceptConnections :182 -> validateConnections :117 -> closeConnection :142,
+# request thread handleRequests server.cpp:355 -> updateActivity :130, and validateConnections' locals
+# fd = 5 (the one client), diff = now = 31030 s (the host's uptime).  The same hang is certain, without
+# any race, for any connection left idle for 300 s.
+REF_CONNECT_RACE = ("reference defect: conn_manager.hpp:83-93 registers the fd with epoll before inserting "
+                    "its ConnectionData, server.cpp:373/:409 read the connections map without conn_mutex")
+REF_SELF_DEADLOCK = ("reference defect: conn_manager.hpp:117 validateConnections calls closeConnection, which "
+                     "relocks conn_mutex (:142), for an entry with lastActivity {0,0} (:58)")
+
+
+def _deadlocked(pid):
+    """Both connection threads of a started server blocked in futex (syscall 202) -- REF_SELF_DEADLOCK."""
+    try:
+        calls = [open(f"/proc/{pid}/task/{t}/syscall").read().split()[0] for t in os.listdir(f"/proc/{pid}/task")]
+    except OSError:
+        return False
+    return calls.count("202") >= 3  # (main's latch wait, the metrics thread's timed wait, and the accept thread)
 
 
 @pytest.mark.parametrize("kind", ["zlib", "dropin", "batch"])
@@ -105,7 +153,7 @@ def test_reference_load_test_passes(kind):
     if not os.path.exists(HARNESS):
         pytest.skip("the reference's harness is only in the build container")
     seen = []
-    for attempt in range(3):
+    for attempt in range(3):  # (RefServer itself restarts a deadlocked server, REF_SELF_DEADLOCK)
         s = RefServer(kind)
         try:
             env = dict(os.environ, CACHE_HOST="127.0.0.1", CACHE_PORT=str(s.port), TEST_DELAY_SEC="0.05",
