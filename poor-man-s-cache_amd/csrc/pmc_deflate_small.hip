@@ -127,6 +127,14 @@ struct FrontLayout {
 #define PMC_FRONT_S10 0
 #endif
 __host__ __device__ inline bool front_s10(uint64_t n) { return PMC_FRONT_S10 && front_pkb(n) == 6; }
+// PMC_SPLIT_MT: at values of <= 1 KiB the split front writes only its matches to the token slab, one
+// 28-bit record each (position << 18 | distance - 1 << 8 | length - 3), and the literals stay implicit
+// (every position no match covers); the front's histogram and the back's emission rebuild them from a
+// coverage bitmap.  The slab shrinks from one word per token to one per match.
+#ifndef PMC_SPLIT_MT
+#define PMC_SPLIT_MT 0
+#endif
+__host__ __device__ inline bool split_mt(uint64_t n) { return PMC_SPLIT_MT && n <= 1024; }
 __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
     auto a = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
     FrontLayout F;
@@ -300,6 +308,13 @@ struct TreeOut {
 #ifndef PMC_PRECAND
 #define PMC_PRECAND 32
 #endif
+// PMC_FRONT_GAP (k > 0): an eval window first compares every position with its nearest chain candidate
+// (16 bytes), follows the lazy parse's likely path through the first k predicted matches and gives no
+// lanes to the positions inside them; the nearest candidate's result seeds each position's maximum, so
+// a position with one candidate needs no lane at all.  0: lanes for every has-candidate position.
+#ifndef PMC_FRONT_GAP
+#define PMC_FRONT_GAP 0
+#endif
 // A uniform 0/1 integer the compiler may not turn back into a bool: branching on it is one
 // s_cmp + s_cbranch_scc.  (Bools merged across blocks become 64-bit lane masks -- s_cselect_b64,
 // s_and_b64 with exec, s_cbranch_vcc -- on the scalar unit, which the parse saturates.)
@@ -315,6 +330,7 @@ struct SmallWave {
     PMC_LDS uint32_t *bw;
     PMC_LDS uint16_t *S, *R;
     uint32_t s10 = 0; // front at <= 1 KiB (front_s10): S packed three 10-bit positions per word (sget)
+    uint32_t mt = 0;  // split front/back at <= 1 KiB (split_mt): the slab holds match records only
     PMC_LDS uint32_t *lfreq, *dfreq, *blfreq;
     PMC_LDS uint32_t *outw;
     PMC_LDS uint8_t *outb;
@@ -919,27 +935,70 @@ struct SmallWave {
         }
         cn = x < npos ? cn : 0u;
         cn1 = x + 1 < npos ? cn1 : 0u;
-        const uint32_t w = SAT && cn == CMAX ? kPreCand : cn < kPreCand ? cn : kPreCand;
+        const uint32_t w0 = SAT && cn == CMAX ? kPreCand : cn < kPreCand ? cn : kPreCand;
+#if PMC_FRONT_GAP
+        // (a) nearest candidate of every offset: q1 = S[R - 1] (a count >= 1 excludes NIL, so the entry
+        // before a position in the hash order is its nearest candidate), 16 bytes compared
+        uint32_t q1 = sget<PK>(cn != 0u ? rx - 1u : 0u);
+        uint64_t X0, X1, Q0, Q1;
+        load16(xc, X0, X1);
+        load16(q1, Q0, Q1);
+        const uint32_t nx1 = (len - xc) < 258 ? (len - xc) : 258;
+        uint32_t f1 = eq_bytes8(X0 ^ Q0);
+        f1 = f1 + (f1 >> 3) * eq_bytes8(X1 ^ Q1);
+        const uint32_t fx = cn != 0u && (f1 < 16u || nx1 <= 16u) ? 1u : 0u; // f1 is q1's exact length
+        f1 = f1 < nx1 ? f1 : nx1;
+        // (b) the lazy parse's likely path from offset 0: at a predicted match j (f1 >= 3, TOO_FAR
+        // respected; j + 1 when that one is longer) the positions j + 2 .. j + f1 - 1 get no lanes
+        const uint64_t jm = ballot(cn != 0u && f1 >= 3u && (f1 > 3u || xc - q1 <= 4096u));
+        uint64_t skip = 0;
+        uint32_t o = 0;
+        for (int it = 0; it < PMC_FRONT_GAP && o < 64; it++) {
+            const uint64_t mj = jm & (~0ull << o);
+            if (!mj) break;
+            uint32_t j = (uint32_t)__builtin_ctzll(mj), fj = readlane(f1, (int)j);
+            if (j < 63 && ((jm >> (j + 1)) & 1)) {
+                const uint32_t fn = readlane(f1, (int)j + 1);
+                j += fn > fj ? 1u : 0u;
+                fj = fn > fj ? fn : fj;
+            }
+            o = j + fj;
+            if (j + 2 < 64) skip |= (o >= 64 ? ~0ull : (1ull << o) - 1) & (~0ull << (j + 2));
+        }
+        const uint32_t sk = (uint32_t)(skip >> l) & 1u;
+        // (c) lanes: the candidates after the nearest where its result is exact
+        const uint32_t w = sk ? 0u : w0 - fx;
+        const bool fre = fx != 0u && w0 == 1u; // one candidate, compared in (a): evaluated without lanes
+#else
+        const uint32_t w = w0, fx = 0;
+        const bool fre = false;
+#endif
         const uint32_t incl = wave_incl_scan_dpp(w), offs = incl - w;
         const bool inc = w != 0 && incl <= 64;
-        const uint64_t im = ballot(inc); // a prefix of the window's has-candidate offsets
-        const uint32_t nl = readlane(incl, 63 - __builtin_clzll(im));
+        const uint64_t iml = ballot(inc); // lane-owning offsets
+        const uint64_t im = iml | ballot(fre); // evaluated offsets
+        const uint32_t nl = iml ? readlane(incl, 63 - __builtin_clzll(iml)) : 0u;
 #ifdef PMC_STAMPS
         st[7] += nl; // (stamps build: lanes used per eval)
 #endif
-        // first lane of each evaluated offset j: offs << 26 | (j + 1) << 19 | R (offs grows
-        // with j, so a max-scan hands every lane its owner); other lanes store to dummy slots
+        // first lane of each evaluated offset j: offs << 26 | (j + 1) << 19 | fx << 18 | R (offs
+        // grows with j, so a max-scan hands every lane its owner); other lanes store to dummy slots
         PMC_LDS uint32_t *dmy = EV + 64; // (the u8 mark area, 16 words)
         EV[l] = 0;
-        (inc ? EV : dmy)[inc ? offs : (l & 15)] = offs << 26 | (l + 1) << 19 | rx;
+        (inc ? EV : dmy)[inc ? offs : (l & 15)] = offs << 26 | (l + 1) << 19 | fx << 18 | rx;
         wave_sync();
         const uint32_t mk = EV[l];
-        EV[l] = 0; // (LDS keeps one wave's accesses in order: the read above sees the marks)
+        // (LDS keeps one wave's accesses in order: the read above sees the marks)
+#if PMC_FRONT_GAP
+        EV[l] = fx ? f1 << 23 | (kPreCand - 1u) << 18 | q1 : 0u; // the nearest candidate's key
+#else
+        EV[l] = 0;
+#endif
         const bool v = l < nl;
         const uint32_t sc = wave_incl_max_dpp(mk);
         const uint32_t own = v ? ((sc >> 19) & 127) - 1 : 0u;
-        const uint32_t P = p0 + own, d = l - (sc >> 26) + 1;
-        const uint32_t rxo = sc & 0x7ffffu;
+        const uint32_t P = p0 + own, d = l - (sc >> 26) + 1 + ((sc >> 18) & 1u);
+        const uint32_t rxo = sc & 0xffffu;
         uint32_t q = sget<PK>(v && (!SAT || rxo >= d) ? rxo - d : 0u);
         uint64_t A0, A1, B0, B1;
         load16(P, A0, A1);
@@ -1050,6 +1109,11 @@ struct SmallWave {
     // stores its run and itself with lane-parallel stores (lane k: token n + k), and the tail run
     // [lf, len) goes out at the end -- no per-literal bookkeeping on the scalar unit.
     __device__ void tb_match(TokBuf &t, uint32_t lf, uint32_t s, uint32_t m) {
+        if (sflag(mt)) { // match record only (m = distance << 16 | length - 3)
+            if (lane_id() == 0) tok[t.n] = s << 18 | ((m >> 16) - 1u) << 8 | (m & 0xffu);
+            t.n++;
+            return;
+        }
         const uint32_t l = (uint32_t)lane_id(), nl = s - lf, cnt = nl + 1;
         // first 64 tokens with every lane storing (no exec mask work on the scalar unit): lanes
         // past the run repeat the match token at its own slot, so no byte past it is written
@@ -1066,6 +1130,7 @@ struct SmallWave {
         t.n += cnt;
     }
     __device__ void tb_lits(TokBuf &t, uint32_t lf, uint32_t e) {
+        if (sflag(mt)) return; // (implicit literals)
         const uint32_t l = (uint32_t)lane_id(), cnt = e - lf;
         for (uint32_t b = 0; b < cnt; b += 64) {
             const uint32_t k = b + l;
@@ -1814,7 +1879,11 @@ struct SmallWave {
 
     // ---- split pipeline pieces (pmc_deflate_split.hip) ----------------------------------------
     // histogram of the token slab into lfreq / dfreq (END_BLOCK counted once)
-    __device__ void histogram(uint32_t ntok) {
+    __device__ void histogram(uint32_t ntok, uint32_t len) {
+        if (sflag(mt)) {
+            histogram_mt(ntok, len);
+            return;
+        }
         const int l = lane_id();
         const Tables &TT = c_tables;
         for (int s = l; s < 352; s += 64) lfreq[s] = 0;
@@ -1830,6 +1899,86 @@ struct SmallWave {
         }
         if (l == 0) lfreq[kEndBlock] = 1;
         wave_sync();
+    }
+    // covered bits [s + skip, s + L) of every match record in the bitmap cov (lds_or per 32-bit word)
+    __device__ void cover_bits(PMC_LDS uint32_t *cov, PMC_LDS uint32_t *starts, uint32_t nm, uint32_t skip) {
+        for (uint32_t t = (uint32_t)lane_id(); t < nm; t += 64) {
+            const uint32_t r = tok[t], st = r >> 18;
+            uint32_t x = st + skip, e = st + (r & 0xffu) + 3u;
+            if (starts) lds_or(&starts[st >> 5], 1u << (st & 31));
+            while (x < e) {
+                const uint32_t b0 = x & 31, n = e - x < 32 - b0 ? e - x : 32 - b0;
+                lds_or(&cov[x >> 5], (n == 32 ? ~0u : (1u << n) - 1u) << b0);
+                x += n;
+            }
+        }
+    }
+    // histogram_mt: the match records' length / distance symbols, and the literal bytes at the
+    // positions no match covers (coverage bitmap in the front's X region, dead after the parse)
+    __device__ void histogram_mt(uint32_t nm, uint32_t len) {
+        const int l = lane_id();
+        PMC_LDS uint32_t *cov = (PMC_LDS uint32_t *)HC;
+        for (int s = l; s < 352; s += 64) lfreq[s] = 0;
+        for (uint32_t k = (uint32_t)l; k < (len + 31) / 32; k += 64) cov[k] = 0;
+        wave_sync();
+        for (uint32_t t = (uint32_t)l; t < nm; t += 64) {
+            const uint32_t r = tok[t];
+            lds_add(&lfreq[len_code_cf(r & 0xffu) + kLiterals + 1], 1u);
+            lds_add(&dfreq[dist_code_cf((r >> 8) & 1023u)], 1u);
+        }
+        cover_bits(cov, nullptr, nm, 0);
+        wave_sync();
+        for (uint32_t p = (uint32_t)l; p < len; p += 64)
+            if (!((cov[p >> 5] >> (p & 31)) & 1u)) lds_add(&lfreq[b[p]], 1u);
+        if (l == 0) lfreq[kEndBlock] = 1;
+        wave_sync();
+    }
+    // emit_symbols over positions (PMC_SPLIT_MT): a literal where no match covers, a match at a record's
+    // start (its record: the starts before it, counted in the start bitmap), nothing inside a match
+    __device__ uint64_t emit_symbols_mt(uint32_t nm, uint32_t len, uint64_t bitpos) {
+        const int l = lane_id();
+        PMC_LDS uint32_t *stb = (PMC_LDS uint32_t *)runs, *cov = stb + 32; // (runs is dead after the headers)
+        stb[l] = 0;
+        wave_sync();
+        cover_bits(cov, stb, nm, 1);
+        wave_sync();
+        uint32_t base = 0;
+        const uint64_t below = (1ull << l) - 1ull;
+        for (uint32_t c0 = 0; c0 < len; c0 += 64) {
+            const uint32_t p = c0 + (uint32_t)l, w = c0 >> 5;
+            const uint64_t sm = (uint64_t)stb[w] | (uint64_t)stb[w + 1] << 32;
+            const uint64_t cm = (uint64_t)cov[w] | (uint64_t)cov[w + 1] << 32;
+            uint32_t nb = 0;
+            uint64_t v = 0;
+            if (p < len) {
+                if ((sm >> l) & 1u) {
+                    const uint32_t r = tok[base + (uint32_t)__builtin_popcountll(sm & below)];
+                    const uint32_t lc = r & 0xffu, code = len_code_cf(lc);
+                    uint32_t c = lcode[code + kLiterals + 1];
+                    v = c & 0xffff;
+                    nb = c >> 16;
+                    const uint32_t xl = len_extra_cf(code);
+                    v |= (uint64_t)((lc - len_base_cf(code)) & ((1u << xl) - 1)) << nb;
+                    nb += xl;
+                    const uint32_t dm = (r >> 8) & 1023u, dc = dist_code_cf(dm);
+                    c = dcode[dc];
+                    v |= (uint64_t)(c & 0xffff) << nb;
+                    nb += c >> 16;
+                    const uint32_t xd = dist_extra_cf(dc);
+                    v |= (uint64_t)((dm - dist_base_cf(dc)) & ((1u << xd) - 1)) << nb;
+                    nb += xd;
+                } else if (!((cm >> l) & 1u)) {
+                    const uint32_t c = lcode[b[p]];
+                    v = c & 0xffff;
+                    nb = c >> 16;
+                }
+            }
+            const uint32_t incl = wave_incl_scan_dpp(nb);
+            if (nb) or_bits_lds(bitpos + incl - nb, v, (int)nb);
+            bitpos += readlane(incl, 63);
+            base += (uint32_t)__builtin_popcountll(sm);
+        }
+        return bitpos;
     }
     // gen_codes (trees.c) for code lengths Ls[0..elems): canonical code = next_code[len] +
     // rank among equal lengths; code_out[s] = bit-reversed code | len << 16 (0: unused)
@@ -2060,7 +2209,7 @@ struct SmallWave {
             wave_sync();
             PMC_STOP(24, bitpos)
         }
-        bitpos = emit_symbols(ntok, bitpos);
+        bitpos = sflag(mt) ? emit_symbols_mt(ntok, len, bitpos) : emit_symbols(ntok, bitpos);
         const uint32_t eob = lcode[kEndBlock];
         wave_sync();
         if (l == 0) or_bits_lds(bitpos, eob & 0xffff, (int)(eob >> 16));
@@ -2138,13 +2287,13 @@ struct SmallWave {
                               : parse_ondemand<0>(npos, len, k0);
             PMC_STOP(14, 0)
             if (sflag(ntok == kNtokRetry ? 1u : 0u)) return kNtokRetry; // (sort guard: no histogram)
-        } else {
-            lit_run(0, 0, len);
-            ntok = len;
+        } else { // (PMC_SPLIT_MT: no match, no record)
+            if (!mt) lit_run(0, 0, len);
+            ntok = mt ? 0u : len;
         }
         wave_sync_global();
         stamp(2);
-        histogram(ntok);
+        histogram(ntok, len);
         stamp(6);
         return ntok;
     }

@@ -44,6 +44,7 @@ __global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kern
     w.EV = to_lds<uint32_t>(base + F.ev);
     w.cnp = F.pkb;
     w.s10 = front_s10(a.cap_len) ? 1u : 0u;
+    w.mt = split_mt(a.cap_len) ? 1u : 0u;
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;
@@ -96,6 +97,11 @@ __global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kern
 }
 
 // ---- trees (one lane per value) ------------------------------------------------------------------
+// PMC_TREES_SKIP: the per-lane symbol loops pass over unused symbols eight at a time (leaf insertion:
+// an all-zero 16-byte group of frequencies; scan_tree: the zero lengths that follow inside a zero run)
+#ifndef PMC_TREES_SKIP
+#define PMC_TREES_SKIP 0
+#endif
 // Packed heap entry, as in the wave kernel: (freq << 5 | depth) << 10 | node, so zlib's
 // smaller(n, m) (freq, then depth, <=) is key(n) <= key(m) with key = entry >> 10.
 template <int CAP>
@@ -169,6 +175,10 @@ struct LaneTrees {
                 }
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
+#if PMC_TREES_SKIP
+                    // (eight unused symbols at once: a JSON value uses none of 0..31 and 127..255)
+                    if ((cur[i].x | cur[i].y | cur[i].z | cur[i].w) == 0u) continue;
+#endif
 #pragma unroll
                     for (int h = 0; h < 8; h++) {
                         const int nn = b * 32 + i * 8 + h;
@@ -351,7 +361,22 @@ struct LaneTrees {
             } else {
                 nextlen = 0xffff;
             }
-            if (++count < max_count && curlen == nextlen) continue;
+            if (++count < max_count && curlen == nextlen) {
+#if PMC_TREES_SKIP
+                // inside a run of zero lengths, the zero bytes after nextlen in the staged word are
+                // iterations that only count (each would take this branch): take them at once
+                if (curlen == 0 && nx - w0 < 7) {
+                    const uint64_t rest = pk >> (8 * (nx - w0 + 1));
+                    uint32_t k = rest ? (uint32_t)__builtin_ctzll(rest) >> 3 : (uint32_t)(7 - (nx - w0));
+                    const uint32_t lim_code = (uint32_t)(max_code - nx), lim_cnt = (uint32_t)(max_count - 1 - count);
+                    k = k < lim_code ? k : lim_code;
+                    k = k < lim_cnt ? k : lim_cnt;
+                    n += (int)k;
+                    count += (int)k;
+                }
+#endif
+                continue;
+            }
             if (count < min_count) {
                 blf[curlen * 64] += count;
             } else if (curlen != 0) {
@@ -479,6 +504,7 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
     w.runs = to_lds<uint16_t>(base + B.runs);
     w.blfreq = to_lds<uint32_t>(base + B.blfreq);
     w.perm = to_lds<uint16_t>(base + B.perm);
+    w.mt = split_mt(a.cap_len) ? 1u : 0u; // (runs holds emit_symbols_mt's bitmaps after the headers)
     // (run_back touches only the arrays above; the rest of w still points into the larger
     // small_layout and must stay unused here)
     PMC_LDS uint8_t *Ls = to_lds<uint8_t>(base + B.ls); // code lengths from the trees kernel
