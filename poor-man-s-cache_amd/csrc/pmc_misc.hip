@@ -103,8 +103,13 @@ __global__ void __launch_bounds__(256) lane_order_probe_kernel(uint32_t trials, 
         const uint32_t d = (x % alpha) & 255u;
         const uint32_t old = lds_add(to_lds<uint32_t>(&tab[w][d >> 1]), 1u << (16 * (d & 1)));
         const uint32_t r = (old >> (16 * (d & 1))) & 0xffffu;
+        // lower lanes with the same digit: each lane's digit by a readlane (uniform, every lane active --
+        // a __shfl under `j < l` would read lane j while it is switched off, and get 0)
         uint32_t want = 0;
-        for (int j = 0; j < 64; j++) want += (j < l && (uint32_t)__shfl((int)d, j) == d) ? 1u : 0u;
+        for (int j = 0; j < 64; j++) {
+            const uint32_t dj = (uint32_t)__builtin_amdgcn_readlane((int)d, j);
+            want += (uint32_t)j < (uint32_t)l && dj == d ? 1u : 0u;
+        }
         bad += r != want ? 1u : 0u;
         wave_sync();
     }
