@@ -358,7 +358,7 @@ def batch_bench(args):
     vlen, reps = args.vlen, 20
     out = []
     corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).to(dev)
-    for n in (256, 1024, 4096, 400):
+    for n in (64, 256, 1024, 4096, 400):
         raw = torch.empty(n * vlen + 16, dtype=torch.uint8, device=dev)
         assert L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), 0x5EED, 0, 0, None, n, vlen, raw.data_ptr(), sh) == 0
         rh = raw.cpu().numpy().tobytes()

@@ -464,11 +464,6 @@ PMC_API uint32_t pmc_gzip_isize(const void *in, size_t in_len) {
 // chain of launches (front, order sort, trees, back; record / lane kernels, CRC verify), which only
 // pays once a batch fills the CUs.
 constexpr uint32_t kLatencyBatch = 64;
-// decompress batches up to this size take the wave-per-member kernels (decompress_batch_body)
-#ifndef PMC_WAVE_INFLATE_BATCH
-#define PMC_WAVE_INFLATE_BATCH 2048
-#endif
-constexpr uint32_t kWaveInflateBatch = PMC_WAVE_INFLATE_BATCH;
 
 // ---- large values (pmc_deflate_large.hip) ------------------------------------------------------------
 // The batch's values of lo < len <= hi.  Their lengths live on the device: one small readback (a count,
@@ -869,11 +864,9 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
     // declines (rc = kInflateRetry) goes through the wave-per-member kernels below
     // (PMC_INFLATE_WAVE=1: everything through the wave kernels).
     static const bool wave_only = getenv("PMC_INFLATE_WAVE") && atoi(getenv("PMC_INFLATE_WAVE"));
-    // Batches of at most kWaveInflateBatch members go to the wave-per-member kernels alone: a member of a few
-    // KiB decodes in tens of microseconds on its own wave, while the lane / record fast paths -- one lane per
-    // member, then a verify pass -- only pay once the members fill the CUs (a 400-member 4 KiB batch took
-    // 3.9 ms through them; round 3).
-    if (!wave_only && !latency && n > kWaveInflateBatch) {
+    // (round 4 measured routing batches of <= 2048 members to the wave kernels instead: 256 x 4 KiB took
+    // 12.5 ms there against 3.2 ms for 4096 members through the lane / record paths -- not done)
+    if (!wave_only && !latency) {
         int r = ctx->crcx.ensure((uint64_t)n * 4);
         if (r) return r;
         a.crc_expect = (uint32_t *)ctx->crcx.p;

@@ -122,7 +122,12 @@ void CacheServer::primeCodecBatch(const std::vector<int> &fds) {
     }
     // the SET batch runs on a helper thread (its own context and stream) while this thread does the GET
     // dry run and the decompress batch: the two device batches overlap
-    if (!set_values.empty()) pmc_batch::PrimeCompressAsync(set_values);
+    // (PMC_HOOK_SYNC=1: the SET batch on this thread first, for comparison)
+    static const bool sync_set = std::getenv("PMC_HOOK_SYNC") && std::atoi(std::getenv("PMC_HOOK_SYNC"));
+    if (!set_values.empty()) {
+        if (sync_set) pmc_batch::PrimeCompress(set_values);
+        else pmc_batch::PrimeCompressAsync(set_values);
+    }
     if (!get_keys.empty()) {
         pmc_batch::BeginCollect();
         for (const std::string &k : get_keys) {

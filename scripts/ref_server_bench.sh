@@ -27,6 +27,10 @@ once() {  # tag cmd... : start a server (cmd), run the load, stop it
     timeout -k 5 240 $B/pmc_loadgen --port $port --data tests/golden/data --vlen $VLEN --ops $OPS --conns $CONNS \
         --keys $KEYS --batch 100 --mix 50 --warmup-sec 10 > "$OUT/load_$tag.json" 2> "$OUT/load_$tag.err"
     local rc=$?
+    if ! kill -0 $pid 2>/dev/null; then  # the server ended under the load: record how
+        wait $pid; echo "server $tag exited with status $? during the load" | tee -a "$OUT/server_$tag.log"
+        return $rc
+    fi
     kill $pid; sleep 2; kill -9 $pid 2>/dev/null; wait $pid 2>/dev/null
     return $rc
 }
@@ -43,12 +47,18 @@ case_() {  # label server-fn kind
     done
     echo "{\"server\": \"$1\", \"failed\": \"no answer after 5 starts\", \"vlen\": $VLEN, \"conns\": $CONNS}" | tee -a "$OUT/ref_server_bench.jsonl"
 }
-for shape in "4096 16 8192 40000" "4096 64 65536 100000" "1024 16 8192 40000"; do
+# (SHAPES / SERVERS narrow the run, e.g. SHAPES="1024 16 8192 40000" SERVERS="ref_batch")
+SERVERS=${SERVERS:-ref_zlib ref_batch pmc_batch ref_dropin}
+want() { case " $SERVERS " in *" $1 "*) return 0 ;; esac; return 1; }
+while read -r shape; do
+    [ -n "$shape" ] || continue
     set -- $shape
     VLEN=$1 CONNS=$2 KEYS=$3 OPS=$4
-    case_ ref_zlib ref_server zlib || exit 1
-    case_ ref_batch ref_server batch || exit 1
-    case_ pmc_batch pmc_srv batch || exit 1
-done
-VLEN=4096 CONNS=16 KEYS=1024 OPS=4000 case_ ref_dropin ref_server dropin
+    if want ref_zlib; then case_ ref_zlib ref_server zlib || exit 1; fi
+    if want ref_batch; then case_ ref_batch ref_server batch || exit 1; fi
+    if want pmc_batch; then case_ pmc_batch pmc_srv batch || exit 1; fi
+done <<< "${SHAPES:-4096 16 8192 40000
+4096 64 65536 100000
+1024 16 8192 40000}"
+if want ref_dropin; then VLEN=4096 CONNS=16 KEYS=1024 OPS=4000 case_ ref_dropin ref_server dropin; fi
 exit 0
