@@ -902,10 +902,15 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
                     nb = (int)(kLdsPerCu / kRecLdsBytes);
                 rec_per_cu = nb;
             }
-            const unsigned rb = (unsigned)std::min<uint64_t>(((uint64_t)n + 63) / 64, (uint64_t)ctx->cus * rec_per_cu);
-            // a batch that cannot fill the CUs once leaves phase B's member-serial wave loop exposed: there,
-            // members of more than 1 KiB output are faster in the lane kernel (all its work lane-parallel)
-            a.rec_max_out = (uint64_t)n >= (uint64_t)ctx->cus * rec_per_cu * 64 ? kRecOutMax : 1024u;
+            // members per grab: the smallest power of two whose grabs fit the resident blocks once, so a small
+            // batch (a server's few hundred GETs) spreads one or a few members per wave instead of 64 on a few
+            // CUs with phase B's member-serial loop exposed
+            const uint64_t slots = (uint64_t)ctx->cus * rec_per_cu;
+            uint32_t G = 1;
+            while (G < 64 && ((uint64_t)n + G - 1) / G > slots) G *= 2;
+            a.rec_group = G;
+            const unsigned rb = (unsigned)std::min<uint64_t>(((uint64_t)n + G - 1) / G, slots);
+            a.rec_max_out = kRecOutMax;
             r = ctx->recs.ensure((uint64_t)rb * 64 * rstride * 4 + 256);
             if (r) return r;
             a.rec_work = (uint32_t *)ctx->recs.p;
@@ -932,7 +937,11 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
                                    a);
         });
         a.big_only = 0;
-        const unsigned vb = (unsigned)std::min<uint64_t>(((uint64_t)n + 511) / 512, (uint64_t)ctx->cus * 4);
+        // (members per wave as for the record kernel: a small batch takes one wave per member)
+        uint32_t VG = 1;
+        while (VG < 64 && ((uint64_t)n + VG - 1) / VG > (uint64_t)ctx->cus * 32) VG *= 2;
+        a.verify_group = VG;
+        const unsigned vb = (unsigned)std::min<uint64_t>(((uint64_t)n + 8ull * VG - 1) / (8ull * VG), (uint64_t)ctx->cus * 4);
         klaunch(ctx, PMC_K_INFLATE_VERIFY, st,
                 [&] { hipLaunchKernelGGL(inflate_verify_kernel, dim3(vb), dim3(512), 0, st, a); });
         a.retry_only = 1;

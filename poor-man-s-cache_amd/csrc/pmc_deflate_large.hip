@@ -168,24 +168,56 @@ __global__ void __launch_bounds__(256) lv_sort_scatter_kernel(LargeArgs a, int p
     }
 }
 
-// R[S[k]] = k and HC[x]: zlib searches at x iff its nearest earlier same-hash position (S[R[x] - 1])
-// exists, is not NIL (position 0) and lies within MAX_DIST (deflate.c: hash_head != NIL &&
-// strstart - hash_head <= MAX_DIST)
+// R[S[k]] = k and HC[x]: 0 if zlib does not search at x, else x's chain length capped at 255 (the
+// same-hash entries before x in S, less NIL position 0, which the stable sort puts first in its run).
+// zlib searches at x iff its nearest earlier same-hash position (S[R[x] - 1]) exists, is not NIL and
+// lies within MAX_DIST (deflate.c: hash_head != NIL && strstart - hash_head <= MAX_DIST).  The count
+// lets the parse's longest_match take the first 255 chain entries without loading their bytes to test
+// the hash.  A chunk's wave carries the run start across its 64-entry steps; the run start of the
+// chunk's first entry is found by looking back up to 256 entries (a longer run caps the count anyway).
 __global__ void __launch_bounds__(256) lv_rank_kernel(LargeArgs a) {
     const uint32_t wib = threadIdx.x / 64, l = (uint32_t)lane_id();
     for (uint64_t c = (uint64_t)blockIdx.x * 4 + wib; c < a.nch; c += (uint64_t)gridDim.x * 4) {
         const uint32_t ov = a.ch_val[c];
         const LvBytes B = lv_bytes(a, ov);
         const LvChunk k = lv_chunk(a, (uint32_t)c, lv_npos(B.len));
-        for (uint32_t x = k.c0 + l; x < k.c1; x += 64) {
-            const uint32_t p = a.S[k.pb + x];
-            a.R[k.pb + p] = x;
-            uint8_t hc = 0;
-            if (x > 0) {
-                const uint32_t q = a.S[k.pb + x - 1];
-                hc = q != 0 && p - q <= kLvMaxDist && lv_hash(B.load4(q)) == lv_hash(B.load4(p)) ? 1 : 0;
+        // run start of entry c0 - 1 (the carry into the first step), or c0 when c0 starts the value
+        uint32_t prs = k.c0, ph = 0xffffffffu;
+        if (k.c0 > 0) {
+            ph = lv_hash(B.load4(a.S[k.pb + k.c0 - 1]));
+            prs = k.c0 >= 257 ? k.c0 - 257 : 0u; // (a run of more than 256 before c0: count >= 255)
+            for (uint32_t b = 0; b < 256 && b < k.c0; b += 64) {
+                const uint32_t y = k.c0 - 1 - b - l; // (entries c0 - 1, c0 - 2, ...)
+                const bool in = b + l < k.c0;
+                const uint64_t m = ballot(in && lv_hash(B.load4(a.S[k.pb + y])) != ph);
+                if (m) {
+                    prs = k.c0 - b - (uint32_t)__builtin_ctzll(m); // (the first entry after the change)
+                    break;
+                }
+                if (b + 64 >= k.c0) prs = 0;
             }
-            a.HC[k.pb + p] = hc;
+        }
+        for (uint32_t x0 = k.c0; x0 < k.c1; x0 += 64) {
+            const uint32_t x = x0 + l;
+            const bool in = x < k.c1;
+            const uint32_t p = in ? a.S[k.pb + x] : 0u;
+            const uint32_t h = in ? lv_hash(B.load4(p)) : 0xfffffffeu;
+            uint32_t hp = (uint32_t)__shfl_up((int)h, 1), qp = (uint32_t)__shfl_up((int)p, 1);
+            if (l == 0) {
+                hp = ph;
+                qp = x > 0 ? a.S[k.pb + x - 1] : 0u;
+            }
+            uint32_t rs = wave_incl_max_dpp(in && h != hp ? x : 0u);
+            rs = rs > prs ? rs : prs;
+            if (in) {
+                a.R[k.pb + p] = x;
+                uint32_t cnt = x - rs;
+                if (cnt && a.S[k.pb + rs] == 0) cnt--; // (NIL heads its run)
+                const bool search = x > 0 && h == hp && qp != 0 && p - qp <= kLvMaxDist;
+                a.HC[k.pb + p] = (uint8_t)(search ? (cnt < 255 ? cnt : 255) : 0);
+            }
+            ph = readlane(h, 63);
+            prs = readlane(rs, 63);
         }
     }
 }
@@ -222,15 +254,18 @@ struct LvParse {
         const uint32_t C = b0 >= 32 ? 1024u : 4096u;
         const uint32_t nice = (len - i) < 258 ? (len - i) : 258;
         const int r = (int)R[pb + i];
-        const uint32_t hi = lv_hash(B.load4(i));
+        const uint32_t cnt = HC[pb + i]; // chain length, 255 = at least 255 (lv_rank_kernel)
+        uint32_t hi = 0;
+        if (cnt == 255) hi = lv_hash(B.load4(i));
         uint32_t best = 0, bestq = 0, examined = 0;
         for (int kb = r - 1;; kb -= 64) {
             const int k = kb - (int)l;
             const uint32_t ord = examined + l;
             const uint32_t q = k >= 0 ? S[pb + (uint32_t)k] : 0u;
             const uint32_t d = i - q;
-            const bool valid = k >= 0 && q != 0 && lv_hash(B.load4(q)) == hi &&
-                               (ord == 0 ? d <= kLvMaxDist : d < kLvMaxDist) && ord < C;
+            // chain membership from the count; past 255 entries by the hash (the run's end)
+            const bool member = ord < cnt || (cnt == 255 && k >= 0 && q != 0 && lv_hash(B.load4(q)) == hi);
+            const bool valid = member && (ord == 0 ? d <= kLvMaxDist : d < kLvMaxDist) && ord < C;
             const uint64_t m = ballot(valid);
             const uint32_t npre = ~m == 0 ? 64u : (uint32_t)__builtin_ctzll(~m);
             if (npre == 0) break;
@@ -268,7 +303,7 @@ __device__ __forceinline__ void lv_state(uint32_t *spec, uint32_t *cont, uint32_
     if (!last && p >= e && p - e < kLvOverlap) cont[p - e] = w;
 }
 
-__global__ void __launch_bounds__(256) lv_parse_kernel(LargeArgs a) {
+__global__ void __launch_bounds__(256, 3) lv_parse_kernel(LargeArgs a) {
     const uint32_t l = (uint32_t)lane_id();
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;

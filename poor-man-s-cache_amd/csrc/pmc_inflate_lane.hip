@@ -869,9 +869,11 @@ __global__ void __launch_bounds__(512) inflate_verify_kernel(InflateArgs a) {
     load_crc_tables(to_lds<uint32_t>(s8), to_lds<uint32_t>(zp));
     const int wpb = blockDim.x / 64, l = lane_id();
     const uint64_t wave = (uint64_t)blockIdx.x * wpb + threadIdx.x / 64, nwaves = (uint64_t)gridDim.x * wpb;
-    for (uint64_t g = wave * 64; g < a.n; g += nwaves * 64) {
+    // (a.verify_group members per wave: a small batch spreads over more waves)
+    const uint32_t G = a.verify_group ? a.verify_group : 64u;
+    for (uint64_t g = wave * G; g < a.n; g += nwaves * G) {
         const uint64_t vl = g + (uint64_t)l;
-        const bool ok = vl < a.n && a.rc[vl] == 0;
+        const bool ok = (uint32_t)l < G && vl < a.n && a.rc[vl] == 0;
         const uint32_t mylen = ok ? a.dst_len[vl] : 0;
         const uint32_t c = wave_crc32_members(a.dst, a.dst_off, g, ballot(ok), mylen, to_lds<const uint32_t>(s8),
                                               to_lds<const uint32_t>(zp));

@@ -150,12 +150,15 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
     PMC_GLB uint32_t *const row = rows + (uint64_t)lane * rstride;
     // 64-member batches from a work counter, the next grab in flight while a batch runs (a block
     // that becomes resident late finds less work instead of adding a tail)
+    // A batch too small to fill the CUs at 64 members per wave grabs fewer (a.rec_group): phase A then
+    // runs on that many lanes and phase B's member-serial loop is that short.
+    const uint32_t G = a.rec_group ? a.rec_group : 64u;
     uint32_t nx = lane == 0 ? atomicAdd(a.rec_work, 1u) : 0u;
     for (;;) {
-        const uint64_t vb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nx, 0) * 64;
+        const uint64_t vb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)nx, 0) * G;
         if (vb >= a.n) break;
         nx = lane == 0 ? atomicAdd(a.rec_work, 1u) : 0u;
-        const uint64_t vi = vb + lane;
+        const uint64_t vi = lane < G ? vb + lane : a.n; // (lanes past the group: no member)
         // (longest members first: batches are handed out in order, so the kernel's last ones are short)
         const uint64_t v = a.order && vi < a.n ? (uint64_t)a.order[a.n - 1 - vi] : vi;
         const uint32_t in_len = v < a.n ? a.src_len[v] : 0u;

@@ -145,6 +145,8 @@ struct InflateArgs {
     uint32_t rec_max_out;  // record kernel: members of more output go to the lane kernel (<= kRecOutMax)
     int32_t multi_pass;    // lane kernel: the multi-block pass runs (mark such members kInflateMulti)
     uint32_t *retried;     // wave kernels in retry_only mode: members they decode are counted here (or null)
+    uint32_t rec_group;    // record kernel: members per grab (a power of two <= 64; 0 = 64)
+    uint32_t verify_group; // verify kernel: members per wave (a power of two <= 64; 0 = 64)
 };
 
 // lane-inflate visit order: member indices grouped by compressed length, so a wave's 64
