@@ -72,6 +72,7 @@ def parse():
     ap.add_argument("--h2h-chunk", type=int, default=0, help="values per chunk of the pipelined h2h leg (0 = n/16)")
     ap.add_argument("--mix", action="store_true",
                     help="BASELINE configs[2]: SET/GET mix over a device-resident compressed store instead")
+    ap.add_argument("--batch-vlen", type=int, default=4096, help="--batches: value bytes (default 4 KiB)")
     ap.add_argument("--batches", action="store_true",
                     help="server-shaped batches (256 / 1,024 / 4,096 / 400 values, default 4 KiB): ms per batch")
     ap.add_argument("--mix-keys", type=int, default=1_000_000)
@@ -358,7 +359,7 @@ def batch_bench(args):
     vlen, reps = args.vlen, 20
     out = []
     corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).to(dev)
-    for n in (64, 256, 1024, 4096, 400):
+    for n in (1, 16, 64, 256, 1024, 4096, 400):
         raw = torch.empty(n * vlen + 16, dtype=torch.uint8, device=dev)
         assert L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), 0x5EED, 0, 0, None, n, vlen, raw.data_ptr(), sh) == 0
         rh = raw.cpu().numpy().tobytes()
@@ -425,8 +426,7 @@ def batch_bench(args):
 def main():
     args = parse()
     if args.batches:
-        if args.vlen == 1024:
-            args.vlen = 4096
+        args.vlen = args.batch_vlen
         return batch_bench(args)
     if args.mix:
         if args.vlen == 1024:

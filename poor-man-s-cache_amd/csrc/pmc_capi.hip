@@ -464,6 +464,7 @@ PMC_API uint32_t pmc_gzip_isize(const void *in, size_t in_len) {
 // chain of launches (front, order sort, trees, back; record / lane kernels, CRC verify), which only
 // pays once a batch fills the CUs.
 constexpr uint32_t kLatencyBatch = 64;
+constexpr uint64_t kLatencyMaxLen = 1024;
 
 // ---- large values (pmc_deflate_large.hip) ------------------------------------------------------------
 // The batch's values of lo < len <= hi.  Their lengths live on the device: one small readback (a count,
@@ -1098,7 +1099,10 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     const uint64_t up = al(n * 4ull) * 2 + al(out_bytes + 16);
     // (values above the small kernels' limit keep the throughput path: the wave-per-value kernel
     // that would take them works from HBM and is far slower than the split pipeline's large pass)
-    const bool latency = n <= kLatencyBatch && (dir == kDecompress || max_len <= deflate_small_limit());
+    // (values of at most kLatencyMaxLen bytes: at 4 KiB the one-kernel paths measured far slower than the
+    // throughput pipeline even for a few values -- 64 x 4 KiB compress 35 ms against 1.7 ms, decompress
+    // 12.4 ms against 0.9 ms, round 4)
+    const bool latency = n <= kLatencyBatch && max_len <= kLatencyMaxLen;
     // The latency path's kernel reads its inputs from, and writes its outputs to, coherent host memory in
     // place: no H2D / D2H copies (each a runtime copy kernel of its own) around its one launch.
     const bool zc = latency;
