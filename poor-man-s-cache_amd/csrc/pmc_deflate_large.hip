@@ -258,10 +258,14 @@ struct LvParse {
         uint32_t hi = 0;
         if (cnt == 255) hi = lv_hash(B.load4(i));
         uint32_t best = 0, bestq = 0, examined = 0;
+        // chain entries one step ahead: the next step's S load is issued with this step's, so its round
+        // trip hides behind this step's byte loads (loads return in order)
+        uint32_t qn = r - 1 - (int)l >= 0 ? S[pb + (uint32_t)(r - 1 - (int)l)] : 0u;
         for (int kb = r - 1;; kb -= 64) {
             const int k = kb - (int)l;
             const uint32_t ord = examined + l;
-            const uint32_t q = k >= 0 ? S[pb + (uint32_t)k] : 0u;
+            const uint32_t q = qn;
+            qn = k - 64 >= 0 ? S[pb + (uint32_t)(k - 64)] : 0u;
             const uint32_t d = i - q;
             // chain membership from the count; past 255 entries by the hash (the run's end)
             const bool member = ord < cnt || (cnt == 255 && k >= 0 && q != 0 && lv_hash(B.load4(q)) == hi);

@@ -315,6 +315,10 @@ struct TreeOut {
 #ifndef PMC_FRONT_GAP
 #define PMC_FRONT_GAP 0
 #endif
+// PMC_LDS_B64: the 16-byte window loads (load16) as three aligned ds_read_b64
+#ifndef PMC_LDS_B64
+#define PMC_LDS_B64 0
+#endif
 // A uniform 0/1 integer the compiler may not turn back into a bool: branching on it is one
 // s_cmp + s_cbranch_scc.  (Bools merged across blocks become 64-bit lane masks -- s_cselect_b64,
 // s_and_b64 with exec, s_cbranch_vcc -- on the scalar unit, which the parse saturates.)
@@ -900,7 +904,22 @@ struct SmallWave {
     // 16 bytes at p as two 8-byte words (5 dword reads + alignbyte)
     __device__ void load16(uint32_t p, uint64_t &lo, uint64_t &hi) const {
         const uint32_t w = p >> 2, sh = p & 3;
+#if PMC_LDS_B64
+        // three 8-byte aligned ds_read_b64 (64 banks, 2 LDS cycles each) instead of five ds_read_b32 (32 banks):
+        // dwords e .. e + 5 of the even e <= w, the five needed picked by w's parity
+        const uint32_t e = w >> 1, od = w & 1u;
+        PMC_LDS const uint64_t *b8 = (PMC_LDS const uint64_t *)bw;
+        // (indices the compiler cannot relate: adjacent ones it merges into ds_read2_b64, 8 LDS cycles for
+        // the two instead of 4)
+        uint32_t e1 = e + 1, e2 = e + 2;
+        asm volatile("" : "+v"(e1), "+v"(e2));
+        const uint64_t x0 = b8[e], x1 = b8[e1], x2 = b8[e2];
+        const uint32_t d0 = (uint32_t)x0, d1 = (uint32_t)(x0 >> 32), d2 = (uint32_t)x1, d3 = (uint32_t)(x1 >> 32);
+        const uint32_t d4 = (uint32_t)x2, d5 = (uint32_t)(x2 >> 32);
+        const uint32_t w0 = od ? d1 : d0, w1 = od ? d2 : d1, w2 = od ? d3 : d2, w3 = od ? d4 : d3, w4 = od ? d5 : d4;
+#else
         const uint32_t w0 = bw[w], w1 = bw[w + 1], w2 = bw[w + 2], w3 = bw[w + 3], w4 = bw[w + 4];
+#endif
         lo = (uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32 | __builtin_amdgcn_alignbyte(w1, w0, sh);
         hi = (uint64_t)__builtin_amdgcn_alignbyte(w4, w3, sh) << 32 | __builtin_amdgcn_alignbyte(w3, w2, sh);
     }

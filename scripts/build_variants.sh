@@ -15,6 +15,8 @@ b libpmc_codec_s10gap.so -DPMC_FRONT_GAP=3 -DPMC_FRONT_S10=1 &
 b libpmc_codec_mt.so -DPMC_SPLIT_MT=1 &
 wait
 b libpmc_codec_tskip.so -DPMC_TREES_SKIP=1 &
+b libpmc_codec_b64.so -DPMC_LDS_B64=1 &
+b libpmc_codec_stop.so -DPMC_PHASE_STOP &
 b libpmc_codec_stamps.so -DPMC_STAMPS &
 b libpmc_codec_stamps_gap.so -DPMC_STAMPS -DPMC_FRONT_GAP=3 &
 wait
