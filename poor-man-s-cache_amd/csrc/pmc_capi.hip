@@ -171,6 +171,7 @@ struct pmc_ctx {
     DevBuf crcx;                 // inflate: CRC-32 trailers from the lane kernel
     DevBuf order;                // inflate: lane visit order (bins | member indices)
     DevBuf recs;                 // inflate: the record kernel's per-lane record rows
+    DevBuf bigl;                 // inflate: count + list of the members the record kernel leaves to the lane kernel
     // lane-order guards (DeflateArgs::guard): u32 [0] sort, [1] code ranks, [2] the create-time probe's
     // violations, [3] values sent to the HBM kernel's retry pass by the other paths, [4] members the
     // decompress fast paths handed to the wave kernels; lane_order_ok = the probe passed (else compress takes the kernels that do not need it)
@@ -409,6 +410,7 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     c->split.release();
     c->crcx.release();
     c->recs.release();
+    c->bigl.release();
     c->guard.release();
     c->lvsel.release();
     c->lvtab.release();
@@ -917,6 +919,11 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
             a.rec_work = (uint32_t *)ctx->recs.p;
             a.rec_scratch = (uint32_t *)((uint8_t *)ctx->recs.p + 256);
             HIP_TRY(hipMemsetAsync(a.rec_work, 0, 4, st));
+            r = ctx->bigl.ensure((uint64_t)n * 4 + 256);
+            if (r) return r;
+            a.big_count = (uint32_t *)ctx->bigl.p;
+            a.big_list = (uint32_t *)((uint8_t *)ctx->bigl.p + 256);
+            HIP_TRY(hipMemsetAsync(a.big_count, 0, 4, st));
             a.rec_stride = rstride;
 #if defined(PMC_STAMPS) || defined(PMC_PHASE_STOP)
             if (const char *e = getenv("PMC_STOP_AFTER")) a.stop_after = atoi(e); // 31 prepare, 32 phase A
@@ -938,6 +945,8 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
                                    a);
         });
         a.big_only = 0;
+        a.big_list = nullptr;
+        a.big_count = nullptr;
         // (members per wave as for the record kernel: a small batch takes one wave per member)
         uint32_t VG = 1;
         while (VG < 64 && ((uint64_t)n + VG - 1) / VG > (uint64_t)ctx->cus * 32) VG *= 2;

@@ -520,9 +520,13 @@ __global__ void __launch_bounds__(64) inflate_lane_kernel(InflateArgs a) {
     PMC_LDS uint32_t *ring = to_lds<uint32_t>((uint8_t *)lcol + LL::kRingOff) + threadIdx.x;
     PMC_LDS uint8_t *bcol = to_lds<uint8_t>((uint8_t *)lcol + (MB ? LL::kBColOff : LL::kRingOff) + threadIdx.x);
     PMC_LDS uint32_t *winw = to_lds<uint32_t>((uint8_t *)lcol + LL::kWinOff) + threadIdx.x;
-    for (uint64_t vb = (uint64_t)blockIdx.x * 64; vb < a.n; vb += (uint64_t)gridDim.x * 64) {
+    // after the record kernel (a.big_list): only the members it left here -- not a pass over all n members
+    // that reads each one's rc and length to skip it (random 4-byte gathers through the visit order)
+    const bool listed = a.big_only && a.big_list;
+    const uint64_t nv = listed ? (uint64_t)*a.big_count : a.n;
+    for (uint64_t vb = (uint64_t)blockIdx.x * 64; vb < nv; vb += (uint64_t)gridDim.x * 64) {
         const uint64_t vi = vb + threadIdx.x;
-        const uint64_t v = a.order && vi < a.n ? (uint64_t)a.order[vi] : vi;
+        const uint64_t v = vi >= nv ? a.n : listed ? (uint64_t)a.big_list[vi] : a.order ? (uint64_t)a.order[vi] : vi;
         const uint32_t in_len = v < a.n ? a.src_len[v] : 0u;
         // st: 0 decoding, 1 end of block reached, 2 declined, 3 no member / empty input, 5 for the wide pass
         uint32_t st = v < a.n ? 0u : 3u;

@@ -316,7 +316,10 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
             }
         }
         if (st == 2) a.rc[v] = kInflateRetry;
-        if (st == 4) a.rc[v] = kInflateBig;
+        if (st == 4) {
+            a.rc[v] = kInflateBig;
+            if (a.big_list) a.big_list[atomicAdd(a.big_count, 1u)] = (uint32_t)v;
+        }
         // ---- phase B: the wave rebuilds each decoded member in LDS and stores it ----
         wave_sync_global(); // rows visible to the whole wave; phase A's LDS is dead from here
 #ifdef PMC_STAMPS

@@ -147,6 +147,8 @@ struct InflateArgs {
     uint32_t *retried;     // wave kernels in retry_only mode: members they decode are counted here (or null)
     uint32_t rec_group;    // record kernel: members per grab (a power of two <= 64; 0 = 64)
     uint32_t verify_group; // verify kernel: members per wave (a power of two <= 64; 0 = 64)
+    uint32_t *big_list;    // record kernel appends the members it leaves to the lane kernel (kInflateBig) here,
+    uint32_t *big_count;   // counted here; the lane passes after it then visit that list only (or null: all n)
 };
 
 // lane-inflate visit order: member indices grouped by compressed length, so a wave's 64
