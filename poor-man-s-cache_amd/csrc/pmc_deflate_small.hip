@@ -333,8 +333,12 @@ struct SmallWave {
     PMC_LDS uint8_t *b;
     PMC_LDS uint32_t *bw;
     PMC_LDS uint16_t *S, *R;
+#if PMC_FRONT_S10
     uint32_t s10 = 0; // front at <= 1 KiB (front_s10): S packed three 10-bit positions per word (sget)
+#endif
+#if PMC_SPLIT_MT
     uint32_t mt = 0;  // split front/back at <= 1 KiB (split_mt): the slab holds match records only
+#endif
     PMC_LDS uint32_t *lfreq, *dfreq, *blfreq;
     PMC_LDS uint32_t *outw;
     PMC_LDS uint8_t *outb;
@@ -355,7 +359,9 @@ struct SmallWave {
     Trees *fb; // HBM scratch for the serial fallback
     PMC_LDS const uint32_t *crc_tab;
     PMC_LDS uint16_t *perm; // split back: the code-rank guard's canonical order (BackLayout::perm)
-    uint32_t fault_rev = 0; // PMC_FAULT_LANE_ORDER builds: this value's sort takes its lanes in reverse
+#ifdef PMC_FAULT_LANE_ORDER
+    uint32_t fault_rev = 0; // this value's sort takes its lanes in reverse (diagnostic build)
+#endif
     static constexpr uint64_t kBitsGuard = ~0ull; // emit_planned: the code-rank guard fired
     uint64_t st[16];
     uint64_t t_last;
@@ -499,7 +505,11 @@ struct SmallWave {
             hiw[l] = c0 | (c0 + u0) << 16;
             wave_sync();
         }
+#if PMC_FRONT_S10
         const uint32_t pk10 = s10; // (packed S: the second scatter ORs 10-bit fields into zeroed words)
+#else
+        constexpr uint32_t pk10 = 0;
+#endif
         for (int pass = 0; pass < 2; pass++) {
             const uint32_t sh = pass ? 8 : 0;
             PMC_LDS uint16_t *dst = pass ? S : Tt;
@@ -1128,11 +1138,13 @@ struct SmallWave {
     // stores its run and itself with lane-parallel stores (lane k: token n + k), and the tail run
     // [lf, len) goes out at the end -- no per-literal bookkeeping on the scalar unit.
     __device__ void tb_match(TokBuf &t, uint32_t lf, uint32_t s, uint32_t m) {
+#if PMC_SPLIT_MT
         if (sflag(mt)) { // match record only (m = distance << 16 | length - 3)
             if (lane_id() == 0) tok[t.n] = s << 18 | ((m >> 16) - 1u) << 8 | (m & 0xffu);
             t.n++;
             return;
         }
+#endif
         const uint32_t l = (uint32_t)lane_id(), nl = s - lf, cnt = nl + 1;
         // first 64 tokens with every lane storing (no exec mask work on the scalar unit): lanes
         // past the run repeat the match token at its own slot, so no byte past it is written
@@ -1149,7 +1161,9 @@ struct SmallWave {
         t.n += cnt;
     }
     __device__ void tb_lits(TokBuf &t, uint32_t lf, uint32_t e) {
+#if PMC_SPLIT_MT
         if (sflag(mt)) return; // (implicit literals)
+#endif
         const uint32_t l = (uint32_t)lane_id(), cnt = e - lf;
         for (uint32_t b = 0; b < cnt; b += 64) {
             const uint32_t k = b + l;
@@ -1899,10 +1913,12 @@ struct SmallWave {
     // ---- split pipeline pieces (pmc_deflate_split.hip) ----------------------------------------
     // histogram of the token slab into lfreq / dfreq (END_BLOCK counted once)
     __device__ void histogram(uint32_t ntok, uint32_t len) {
+#if PMC_SPLIT_MT
         if (sflag(mt)) {
             histogram_mt(ntok, len);
             return;
         }
+#endif
         const int l = lane_id();
         const Tables &TT = c_tables;
         for (int s = l; s < 352; s += 64) lfreq[s] = 0;
@@ -2112,7 +2128,6 @@ struct SmallWave {
     __device__ __noinline__ uint32_t codes_from_lengths_all(PMC_LDS const uint8_t *Ls, PMC_LDS uint32_t *code0,
                                                             PMC_LDS uint32_t *tmp, PMC_LDS uint16_t *perm) {
         constexpr int E = kLCodes + kDCodes + kBLCodes;
-        constexpr int NC = (E + 63) / 64;
         const uint32_t l = (uint32_t)lane_id();
 #ifdef PMC_FAULT_LANE_ORDER
         const uint32_t lo = 63u - l;
@@ -2122,16 +2137,15 @@ struct SmallWave {
         for (uint32_t k = l; k < 96; k += 64) tmp[k] = 0;
         wave_sync();
         auto tree_of = [](int s) { return s < kLCodes ? 0u : s < kLCodes + kDCodes ? 1u : 2u; };
-        uint32_t rk[NC];
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-            const int s = 64 * c + (int)lo;
+        for (int c0 = 0; c0 < E; c0 += 64) {
+            const int s = c0 + (int)lo;
             const bool in = s < E;
             const uint32_t len = in ? Ls[s] : 0u, t = tree_of(s), key = t << 4 | len;
             // the symbol's rank among the earlier ones of its (tree, length): one returning LDS
             // atomic (the lanes of one instruction get their old counts in lane order, and one
-            // wave's atomics apply in order across chunks; scripts/micro/lds_atomic_order.hip)
-            rk[c] = in && len ? lds_add(&tmp[key], 1u) : 0u;
+            // wave's atomics apply in order across chunks; scripts/micro/lds_atomic_order.hip),
+            // parked in its code slot (slots: s, 288 + s - 286, 320 + s - 316)
+            if (in) code0[s + 2 * t] = len ? lds_add(&tmp[key], 1u) : 0u;
         }
         wave_sync();
         {
@@ -2153,28 +2167,36 @@ struct SmallWave {
             }
         }
         wave_sync();
-        uint32_t pj[NC];
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-            const int s = 64 * c + (int)lo;
-            pj[c] = 0;
+        // codes; each symbol's canonical position (its tree's base + the symbols with shorter codes +
+        // its rank) gets the symbol in perm
+        for (int c0 = 0; c0 < E; c0 += 64) {
+            const int s = c0 + (int)lo;
             if (s < E) {
                 const uint32_t len = Ls[s], t = tree_of(s), slot = (uint32_t)s + 2 * t, key = t << 4 | len;
-                const uint32_t mycode = tmp[48 + key] + rk[c];
+                const uint32_t rk = code0[slot], mycode = tmp[48 + key] + rk;
                 code0[slot] = len ? ((__builtin_bitreverse32(mycode) >> (32 - len)) | (len << 16)) : 0u;
-                // canonical position, 1-based (0: no code); trees at perm 0 / 286 / 316
-                pj[c] = len ? (uint32_t)(t == 0 ? 0 : t == 1 ? kLCodes : kLCodes + kDCodes) + tmp[96 + key] + rk[c] + 1
-                            : 0u;
-                if (len) perm[pj[c] - 1] = (uint16_t)s;
+                if (len)
+                    perm[(t == 0 ? 0u : t == 1 ? (uint32_t)kLCodes : (uint32_t)(kLCodes + kDCodes)) + tmp[96 + key] + rk] =
+                        (uint16_t)s;
             }
         }
         wave_sync();
+        // the guard: a symbol of rank > 0 must follow a smaller symbol of its (tree, length) in perm.  The
+        // rank comes back from the code (the canonical code minus the length's first code), so nothing is
+        // held in registers across the passes.
         uint32_t bad = 0;
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-            const int s = 64 * c + (int)lo;
-            // rank > 0: the previous canonical position holds this (tree, length)'s previous symbol
-            if (pj[c] && rk[c]) bad |= perm[pj[c] - 2] >= (uint32_t)s ? 1u : 0u;
+        for (int c0 = 0; c0 < E; c0 += 64) {
+            const int s = c0 + (int)lo;
+            if (s < E) {
+                const uint32_t len = Ls[s], t = tree_of(s), key = t << 4 | len;
+                if (len) {
+                    const uint32_t code = code0[(uint32_t)s + 2 * t] & 0xffffu;
+                    const uint32_t rk = (__builtin_bitreverse32(code) >> (32 - len)) - tmp[48 + key];
+                    const uint32_t pj = (t == 0 ? 0u : t == 1 ? (uint32_t)kLCodes : (uint32_t)(kLCodes + kDCodes)) +
+                                        tmp[96 + key] + rk;
+                    if (rk) bad |= perm[pj - 1] >= (uint32_t)s ? 1u : 0u;
+                }
+            }
         }
         return ballot(bad != 0u) ? 1u : 0u;
     }
@@ -2228,7 +2250,11 @@ struct SmallWave {
             wave_sync();
             PMC_STOP(24, bitpos)
         }
+#if PMC_SPLIT_MT
         bitpos = sflag(mt) ? emit_symbols_mt(ntok, len, bitpos) : emit_symbols(ntok, bitpos);
+#else
+        bitpos = emit_symbols(ntok, bitpos);
+#endif
         const uint32_t eob = lcode[kEndBlock];
         wave_sync();
         if (l == 0) or_bits_lds(bitpos, eob & 0xffff, (int)(eob >> 16));
@@ -2306,9 +2332,14 @@ struct SmallWave {
                               : parse_ondemand<0>(npos, len, k0);
             PMC_STOP(14, 0)
             if (sflag(ntok == kNtokRetry ? 1u : 0u)) return kNtokRetry; // (sort guard: no histogram)
-        } else { // (PMC_SPLIT_MT: no match, no record)
+        } else {
+#if PMC_SPLIT_MT // (no match, no record)
             if (!mt) lit_run(0, 0, len);
             ntok = mt ? 0u : len;
+#else
+            lit_run(0, 0, len);
+            ntok = len;
+#endif
         }
         wave_sync_global();
         stamp(2);

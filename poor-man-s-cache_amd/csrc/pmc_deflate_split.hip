@@ -43,8 +43,12 @@ __global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kern
     w.HC = to_lds<uint64_t>(base + F.hc);
     w.EV = to_lds<uint32_t>(base + F.ev);
     w.cnp = F.pkb;
+#if PMC_FRONT_S10
     w.s10 = front_s10(a.cap_len) ? 1u : 0u;
+#endif
+#if PMC_SPLIT_MT
     w.mt = split_mt(a.cap_len) ? 1u : 0u;
+#endif
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;
@@ -504,7 +508,9 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
     w.runs = to_lds<uint16_t>(base + B.runs);
     w.blfreq = to_lds<uint32_t>(base + B.blfreq);
     w.perm = to_lds<uint16_t>(base + B.perm);
+#if PMC_SPLIT_MT
     w.mt = split_mt(a.cap_len) ? 1u : 0u; // (runs holds emit_symbols_mt's bitmaps after the headers)
+#endif
     // (run_back touches only the arrays above; the rest of w still points into the larger
     // small_layout and must stay unused here)
     PMC_LDS uint8_t *Ls = to_lds<uint8_t>(base + B.ls); // code lengths from the trees kernel
