@@ -315,6 +315,10 @@ struct TreeOut {
 #ifndef PMC_FRONT_GAP
 #define PMC_FRONT_GAP 0
 #endif
+// PMC_SORT_U32: the hash sort's digit counters one u32 per digit (sort_positions2_body)
+#ifndef PMC_SORT_U32
+#define PMC_SORT_U32 0
+#endif
 // PMC_LDS_B64: the 16-byte window loads (load16) as three aligned ds_read_b64
 #ifndef PMC_LDS_B64
 #define PMC_LDS_B64 0
@@ -477,6 +481,60 @@ struct SmallWave {
         // shorter values count per pass.)
         PMC_LDS uint32_t *hiw = (PMC_LDS uint32_t *)S;
         const bool fused = npos >= 128;
+#if PMC_SORT_U32
+        // PMC_SORT_U32: one u32 counter per digit instead of two u16 per word (digits d and d ^ 1 no longer
+        // share an address, so fewer lanes of a returning atomic serialise on one word): the 256 low-digit
+        // counters in S (free until the second scatter), the 128 high-digit ones in tab
+        // (values of 512 .. 1024 bytes: S then spans at least 1 KiB, the cap's 2 * cap + 2 bytes)
+        if (!PMC_FRONT_S10 && npos >= 510 && npos <= 1022) {
+            PMC_LDS uint32_t *cl = (PMC_LDS uint32_t *)S;
+            for (uint32_t k = l; k < 256; k += 64) cl[k] = 0;
+            for (uint32_t k = l; k < 128; k += 64) tab[k] = 0;
+            wave_sync();
+            for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+                const uint32_t x = c0 + l;
+                const uint32_t h = hash3(load4(x < npos ? x : 0u));
+                k0 += (uint32_t)__builtin_popcountll(ballot(x < npos && h < h0));
+                if (x < npos) {
+                    lds_add(&cl[h & 255], 1u);
+                    lds_add(&tab[(h >> 8) & 127], 1u);
+                }
+            }
+            wave_sync();
+            { // exclusive bases: 4 low counters per lane, 2 high ones per lane
+                uint32_t v[4], sum = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) sum += (v[k] = cl[4 * l + k]);
+                uint32_t b = wave_incl_scan_dpp(sum) - sum;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    cl[4 * l + k] = b;
+                    b += v[k];
+                }
+                const uint32_t h0c = tab[2 * l], h1c = tab[2 * l + 1], hs = h0c + h1c;
+                const uint32_t hb = wave_incl_scan_dpp(hs) - hs;
+                tab[2 * l] = hb;
+                tab[2 * l + 1] = hb + h0c;
+            }
+            wave_sync();
+            for (int pass = 0; pass < 2; pass++) {
+                PMC_LDS uint32_t *ctr = pass ? tab : cl;
+                PMC_LDS uint16_t *dst = pass ? S : Tt;
+                for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+#ifdef PMC_FAULT_LANE_ORDER
+                    const uint32_t x = fault_rev ? c0 + 63u - l : c0 + l;
+#else
+                    const uint32_t x = c0 + l;
+#endif
+                    const uint32_t p = x < npos ? (pass ? (uint32_t)Tt[x] : x) : 0u;
+                    const uint32_t h = hash3(load4(p)), d = pass ? (h >> 8) & 127 : h & 255;
+                    if (x < npos) dst[lds_add(&ctr[d], 1u)] = (uint16_t)p;
+                }
+                wave_sync();
+            }
+            return k0;
+        }
+#endif
         auto scan_tab = [&]() { // 256 counters -> exclusive bases
             const uint32_t t0 = tab[2 * l], t1 = tab[2 * l + 1];
             const uint32_t v0 = t0 & 0xffffu, v1 = t0 >> 16, v2 = t1 & 0xffffu, v3 = t1 >> 16;
@@ -531,7 +589,7 @@ struct SmallWave {
                 scan_tab();
                 wave_sync();
             }
-            if (pass && pk10) {
+            if ((uint32_t)pass & pk10) {
                 for (uint32_t k = l; k < (npos + 2) / 3; k += 64) ((PMC_LDS uint32_t *)S)[k] = 0u;
                 wave_sync();
             }
@@ -549,7 +607,7 @@ struct SmallWave {
                 const uint32_t d = (hash3(load4(p)) >> sh) & 255, hs = 16 * (d & 1);
                 if (x < npos) {
                     const uint32_t slot = (lds_add(&tab[d >> 1], 1u << hs) >> hs) & 0xffffu;
-                    if (pass && pk10) {
+                    if ((uint32_t)pass & pk10) {
                         const uint32_t w = __umul24(slot, 0xAAABu) >> 17;
                         lds_or((PMC_LDS uint32_t *)S + w, p << (10 * (slot - 3 * w)));
                     } else {
