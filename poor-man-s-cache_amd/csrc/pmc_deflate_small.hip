@@ -315,6 +315,10 @@ struct TreeOut {
 #ifndef PMC_FRONT_GAP
 #define PMC_FRONT_GAP 0
 #endif
+// PMC_EVAL_SEGMAX: at <= 1 KiB the eval's per-position maximum by a segmented max-scan, not LDS atomics
+#ifndef PMC_EVAL_SEGMAX
+#define PMC_EVAL_SEGMAX 0
+#endif
 // PMC_SORT_U32: the hash sort's digit counters one u32 per digit (sort_positions2_body)
 #ifndef PMC_SORT_U32
 #define PMC_SORT_U32 0
@@ -1122,8 +1126,24 @@ struct SmallWave {
             off += 16;
         }
         cl = cl < nice ? cl : nice;
-        __hip_atomic_fetch_max(&EV[own], vk ? cl << 23 | (kPreCand - d) << 18 | q : 0u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+#if PMC_EVAL_SEGMAX
+        if constexpr (PK == 6) {
+            // an offset's lanes are contiguous and own grows with the lane: an inclusive max-scan of
+            // own << 24 | (cl, nearness, q) leaves each offset's maximum in its last lane, which stores it --
+            // no same-address atomics (positions < 1024 at this size, so q takes 10 bits)
+            const uint32_t k2 = own << 24 | (vk ? cl << 15 | (kPreCand - d) << 10 | q : 0u);
+            const uint32_t mx = wave_incl_max_dpp(k2);
+            const uint32_t onx = (uint32_t)__builtin_amdgcn_update_dpp(64, (int)own, 0x130, 0xf, 0xf, false); // lane l + 1
+            if (v && (l + 1 >= nl || onx != own)) {
+                const uint32_t m = mx & 0xffffffu;
+                EV[own] = (m >> 15) << 23 | ((m >> 10) & 31u) << 18 | (m & 1023u);
+            }
+        } else
+#endif
+        {
+            __hip_atomic_fetch_max(&EV[own], vk ? cl << 23 | (kPreCand - d) << 18 | q : 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
         wave_sync();
         const uint32_t kk = EV[l], best = kk >> 23;
         const uint32_t nx = (len - x) < 258 ? (len - x) : 258;
