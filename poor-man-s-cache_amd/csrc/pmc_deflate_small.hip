@@ -315,13 +315,13 @@ struct TreeOut {
 #ifndef PMC_FRONT_GAP
 #define PMC_FRONT_GAP 0
 #endif
-// PMC_EVAL_SEGMAX: at <= 1 KiB the eval's per-position maximum by a segmented max-scan, not LDS atomics
+// PMC_EVAL_SEGMAX: at <= 4 KiB the eval's per-position maximum by a segmented max-scan, not LDS atomics
 #ifndef PMC_EVAL_SEGMAX
-#define PMC_EVAL_SEGMAX 0
+#define PMC_EVAL_SEGMAX 1
 #endif
 // PMC_SORT_U32: the hash sort's digit counters one u32 per digit (sort_positions2_body)
 #ifndef PMC_SORT_U32
-#define PMC_SORT_U32 0
+#define PMC_SORT_U32 1
 #endif
 // PMC_LDS_B64: the 16-byte window loads (load16) as three aligned ds_read_b64
 #ifndef PMC_LDS_B64
@@ -1127,16 +1127,17 @@ struct SmallWave {
         }
         cl = cl < nice ? cl : nice;
 #if PMC_EVAL_SEGMAX
-        if constexpr (PK == 6) {
-            // an offset's lanes are contiguous and own grows with the lane: an inclusive max-scan of
-            // own << 24 | (cl, nearness, q) leaves each offset's maximum in its last lane, which stores it --
-            // no same-address atomics (positions < 1024 at this size, so q takes 10 bits)
-            const uint32_t k2 = own << 24 | (vk ? cl << 15 | (kPreCand - d) << 10 | q : 0u);
+        if (sflag(len <= 4096 ? 1u : 0u)) {
+            // An offset's lanes are contiguous and own grows with the lane: an inclusive max-scan of
+            // own << 26 | (cl, nearness, q) leaves each offset's maximum in its last lane, which stores it.
+            // No same-address LDS atomics: the lanes of one position used to serialise on its word (round 4:
+            // front 194 -> 185 ms at 1 KiB).  Positions < 4096 at these sizes, so q takes 12 bits.
+            const uint32_t k2 = own << 26 | (vk ? cl << 17 | (kPreCand - d) << 12 | q : 0u);
             const uint32_t mx = wave_incl_max_dpp(k2);
             const uint32_t onx = (uint32_t)__builtin_amdgcn_update_dpp(64, (int)own, 0x130, 0xf, 0xf, false); // lane l + 1
             if (v && (l + 1 >= nl || onx != own)) {
-                const uint32_t m = mx & 0xffffffu;
-                EV[own] = (m >> 15) << 23 | ((m >> 10) & 31u) << 18 | (m & 1023u);
+                const uint32_t m = mx & 0x3ffffffu;
+                EV[own] = (m >> 17) << 23 | ((m >> 12) & 31u) << 18 | (m & 4095u);
             }
         } else
 #endif
