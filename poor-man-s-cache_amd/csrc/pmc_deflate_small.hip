@@ -319,6 +319,10 @@ struct TreeOut {
 #ifndef PMC_EVAL_SEGMAX
 #define PMC_EVAL_SEGMAX 1
 #endif
+// PMC_SORT_AGG: (with PMC_SORT_U32) the chunk's lanes sharing lane 0's digit take one atomic together
+#ifndef PMC_SORT_AGG
+#define PMC_SORT_AGG 0
+#endif
 // PMC_SORT_U32: the hash sort's digit counters one u32 per digit (sort_positions2_body)
 #ifndef PMC_SORT_U32
 #define PMC_SORT_U32 1
@@ -495,14 +499,30 @@ struct SmallWave {
             for (uint32_t k = l; k < 256; k += 64) cl[k] = 0;
             for (uint32_t k = l; k < 128; k += 64) tab[k] = 0;
             wave_sync();
+            // (PMC_SORT_AGG: lane 0's digit is taken once for all the chunk's lanes that share it -- runs of
+            // one byte, JSON indentation, put many lanes of an instruction on one counter, and the LDS
+            // serialises same-address atomics)
+            const uint64_t below = (1ull << l) - 1ull;
+            auto agg_add = [&](PMC_LDS uint32_t *ctr, uint32_t d, bool valid) -> uint32_t {
+#if PMC_SORT_AGG
+                const uint32_t d0 = readlane(d, 0);
+                const uint64_t m = ballot(valid && d == d0);
+                const bool inm = (m >> l) & 1ull;
+                const uint32_t lead = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+                uint32_t old = 0;
+                if (valid && (!inm || l == lead)) old = lds_add(&ctr[d], inm ? (uint32_t)__builtin_popcountll(m) : 1u);
+                const uint32_t base = readlane(old, (int)lead);
+                return inm ? base + (uint32_t)__builtin_popcountll(m & below) : old;
+#else
+                return valid ? lds_add(&ctr[d], 1u) : 0u;
+#endif
+            };
             for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
                 const uint32_t x = c0 + l;
                 const uint32_t h = hash3(load4(x < npos ? x : 0u));
                 k0 += (uint32_t)__builtin_popcountll(ballot(x < npos && h < h0));
-                if (x < npos) {
-                    lds_add(&cl[h & 255], 1u);
-                    lds_add(&tab[(h >> 8) & 127], 1u);
-                }
+                agg_add(cl, h & 255, x < npos);
+                agg_add(tab, (h >> 8) & 127, x < npos);
             }
             wave_sync();
             { // exclusive bases: 4 low counters per lane, 2 high ones per lane
@@ -532,7 +552,8 @@ struct SmallWave {
 #endif
                     const uint32_t p = x < npos ? (pass ? (uint32_t)Tt[x] : x) : 0u;
                     const uint32_t h = hash3(load4(p)), d = pass ? (h >> 8) & 127 : h & 255;
-                    if (x < npos) dst[lds_add(&ctr[d], 1u)] = (uint16_t)p;
+                    const uint32_t slot = agg_add(ctr, d, x < npos);
+                    if (x < npos) dst[slot] = (uint16_t)p;
                 }
                 wave_sync();
             }
