@@ -319,6 +319,10 @@ struct TreeOut {
 #ifndef PMC_EVAL_SEGMAX
 #define PMC_EVAL_SEGMAX 1
 #endif
+// PMC_HC_BALLOT: build_cn writes the has-candidate bits by a ballot pass over the counts, not lds_or
+#ifndef PMC_HC_BALLOT
+#define PMC_HC_BALLOT 0
+#endif
 // PMC_SORT_AGG: (with PMC_SORT_U32) the chunk's lanes sharing lane 0's digit take one atomic together
 #ifndef PMC_SORT_AGG
 #define PMC_SORT_AGG 0
@@ -945,8 +949,11 @@ struct SmallWave {
         const uint32_t l = (uint32_t)lane_id();
         // has-candidate bits set by position below (HC as u32 words, LDS atomics): no second
         // pass over the positions
-        for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
-        wave_sync();
+        constexpr bool kHcPass = PMC_HC_BALLOT && PK >= 0; // (HC from the counts afterwards, by ballot)
+        if (!kHcPass) {
+            for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
+            wave_sync();
+        }
         uint32_t ph = 0xffffffffu, prs = 0, pq = 0; // previous chunk's last hash, run start, position
         uint32_t bad = 0;
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
@@ -965,13 +972,24 @@ struct SmallWave {
             if (valid) { // (the rank array R is written here, not by the sort)
                 R[p] = (uint16_t)(PK > 0 ? k | (cnt < CMAX ? cnt : CMAX) << RB : k);
                 if (PK == 0) CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
-                if (cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
+                if (!kHcPass && cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
             }
             ph = readlane(h, 63);
             prs = readlane(rs, 63);
             pq = readlane(p, 63);
         }
         wave_sync();
+        if constexpr (kHcPass) {
+            // has-candidate bits in position order: a ballot of the counts per 64 positions, stored by one
+            // lane (no same-word atomics from lanes of one hash run)
+            for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+                const uint32_t x = c0 + l;
+                const uint32_t c = x < npos ? (PK > 0 ? (uint32_t)R[x] >> RB : (uint32_t)CN[x]) : 0u;
+                const uint64_t m = ballot(c != 0u);
+                if (l == 0) HC[c0 >> 6] = m;
+            }
+            wave_sync();
+        }
         return ballot(bad != 0u) ? 1u : 0u;
     }
     // results of the current eval: window start p0, evaluated offsets m (uniform) and, in
