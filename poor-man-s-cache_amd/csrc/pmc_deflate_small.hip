@@ -319,6 +319,13 @@ struct TreeOut {
 #ifndef PMC_EVAL_SEGMAX
 #define PMC_EVAL_SEGMAX 1
 #endif
+// PMC_FRONT_INLINE: the sort and the parse inlined into their kernels (the wave state then never lives in
+// scratch) instead of noinline calls that copy it from there
+#if defined(PMC_FRONT_INLINE) && PMC_FRONT_INLINE
+#define PMC_NOINLINE_FRONT __forceinline__
+#else
+#define PMC_NOINLINE_FRONT __noinline__
+#endif
 // PMC_HC_BALLOT: build_cn writes the has-candidate bits by a ballot pass over the counts, not lds_or
 #ifndef PMC_HC_BALLOT
 #define PMC_HC_BALLOT 0
@@ -476,7 +483,7 @@ struct SmallWave {
     // the scatter is stable without per-lane counters or a ballot per digit bit.
     // Returns the rank of position 0 (the number of positions whose hash is smaller: the sort is
     // stable and 0 is the lowest position); the rank array R itself is written by build_cn.
-    __device__ __noinline__ uint32_t sort_positions2(uint32_t npos_, PMC_LDS uint32_t *tab) {
+    __device__ PMC_NOINLINE_FRONT uint32_t sort_positions2(uint32_t npos_, PMC_LDS uint32_t *tab) {
         SmallWave me = *this; // (see parse_ondemand)
         return me.sort_positions2_body(npos_, tab);
     }
@@ -1304,7 +1311,7 @@ struct SmallWave {
     // member pointer would be re-read from memory inside the loop.  A local copy lives in SGPRs.)
     template <int PK>
     // (k0_: the rank of position 0, from sort_positions2; build_cn needs it before R exists)
-    __device__ __noinline__ uint32_t parse_ondemand(uint32_t npos_, uint32_t len_, uint32_t k0_) {
+    __device__ PMC_NOINLINE_FRONT uint32_t parse_ondemand(uint32_t npos_, uint32_t len_, uint32_t k0_) {
         SmallWave me = *this;
         const uint32_t r = me.parse_ondemand_body<PK>(npos_, len_, k0_);
 #ifdef PMC_STAMPS

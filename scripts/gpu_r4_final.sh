@@ -18,5 +18,7 @@ tail -2 $O/round_pmc.log
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
 cut -c1-400 $O/bench.json
 timeout -k 10 300 python bench.py --batches > $O/batches.json 2> $O/batches.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_batches -o run --output-format csv \
+    -- python3 bench.py --batches > $O/batches_traced.json 2> $O/batches_traced.err || exit $?
 TAG=$T/b64 LIBS="libpmc_codec.so libpmc_codec_b64.so" bash scripts/gpu_variants.sh
 exit 0
