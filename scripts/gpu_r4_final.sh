@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4 artifacts from the final tree: the whole -m gpu suite, smoke(), the kernel-trace summary of the
 # default bench, the PMC traffic passes (profiles/r04/traffic.json, stamped with the sources' id), the
-# default bench with that roofline, the server-shaped batch leg; then a last A/B (PMC_LDS_B64).
+# default bench with that roofline, the server-shaped batch leg and its kernel trace.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 T=${TAG:-r4final}
@@ -20,5 +20,4 @@ cut -c1-400 $O/bench.json
 timeout -k 10 300 python bench.py --batches > $O/batches.json 2> $O/batches.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_batches -o run --output-format csv \
     -- python3 bench.py --batches > $O/batches_traced.json 2> $O/batches_traced.err || exit $?
-TAG=$T/b64 LIBS="libpmc_codec.so libpmc_codec_b64.so" bash scripts/gpu_variants.sh
 exit 0
