@@ -47,10 +47,10 @@ class RefServer:
         # accept thread starts, all inside REF_CONNECT_RACE's window.  So no connection is made before
         # Start() has printed its ready line (server.cpp:645, flushed by std::endl); then a throwaway GET
         # is retried on fresh connections until answered.  A start whose first connection hits
-        # REF_SELF_DEADLOCK never answers anything: it is killed and the server started again, up to five
-        # times (about half of all starts deadlock on this host); five dead starts xfail with the citation.
+        # REF_SELF_DEADLOCK never answers anything: it is killed and the server started again, up to eight
+        # times (about half of all starts deadlock on this host); eight dead starts xfail with the citation.
         self.exe, self.env, self.starts = exe, env, []
-        for attempt in range(5):
+        for attempt in range(8):
             if self._start():
                 return
         pytest.xfail(f"{REF_SELF_DEADLOCK}; {len(self.starts)} starts: {self.starts}")
