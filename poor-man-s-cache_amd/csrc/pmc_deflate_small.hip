@@ -330,10 +330,6 @@ struct TreeOut {
 #else
 #define PMC_NOINLINE_FRONT __noinline__
 #endif
-// PMC_CODES_BALLOT: canonical-code ranks in the back from match masks (ballots), not returning LDS atomics
-#ifndef PMC_CODES_BALLOT
-#define PMC_CODES_BALLOT 0
-#endif
 // PMC_HC_BALLOT: build_cn writes the has-candidate bits by a ballot pass over the counts, not lds_or
 #ifndef PMC_HC_BALLOT
 #define PMC_HC_BALLOT 0
@@ -2274,34 +2270,11 @@ struct SmallWave {
             const int s = c0 + (int)lo;
             const bool in = s < E;
             const uint32_t len = in ? Ls[s] : 0u, t = tree_of(s), key = t << 4 | len;
-#if PMC_CODES_BALLOT
-            // the symbol's rank among the earlier ones of its (tree, length): the earlier chunks' count
-            // (tmp[key], read by every lane of the key at once) plus the lanes below with the same key
-            // (a match mask from six ballots of the key's bits); the key's highest lane stores the new
-            // count.  No returning atomics: the lanes of one length no longer serialise on its counter,
-            // and nothing depends on the order in which the LDS answers them.
-            const bool has = in && len != 0u;
-            uint64_t m = ballot(has);
-#pragma unroll
-            for (int b = 0; b < 6; b++) {
-                const uint32_t bit = (key >> b) & 1u;
-                const uint64_t bb = ballot(bit != 0u);
-                m &= bit ? bb : ~bb;
-            }
-            const uint32_t base = has ? tmp[key] : 0u;
-            const uint64_t below = (1ull << l) - 1ull;
-            const uint32_t rk = base + (uint32_t)__builtin_popcountll(m & below);
-            wave_sync();
-            if (has && (m >> l) == 1ull) tmp[key] = base + (uint32_t)__builtin_popcountll(m); // (highest lane)
-            if (in) code0[s + 2 * t] = has ? rk : 0u;
-            wave_sync();
-#else
             // the symbol's rank among the earlier ones of its (tree, length): one returning LDS
             // atomic (the lanes of one instruction get their old counts in lane order, and one
             // wave's atomics apply in order across chunks; scripts/micro/lds_atomic_order.hip),
             // parked in its code slot (slots: s, 288 + s - 286, 320 + s - 316)
             if (in) code0[s + 2 * t] = len ? lds_add(&tmp[key], 1u) : 0u;
-#endif
         }
         wave_sync();
         {
@@ -2337,9 +2310,6 @@ struct SmallWave {
             }
         }
         wave_sync();
-#if PMC_CODES_BALLOT && !defined(PMC_FAULT_LANE_ORDER)
-        return 0u; // (ballot ranks: canonical by construction, no lane-order assumption to guard)
-#endif
         // the guard: a symbol of rank > 0 must follow a smaller symbol of its (tree, length) in perm.  The
         // rank comes back from the code (the canonical code minus the length's first code), so nothing is
         // held in registers across the passes.
