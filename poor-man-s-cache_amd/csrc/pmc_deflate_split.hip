@@ -28,10 +28,6 @@ namespace pmc {
 // interleaved by 64-value block (lane-coalesced).
 
 // ---- front -------------------------------------------------------------------------------------
-// PMC_FRONT_PF: L2 prefetch of the next value of the grab while this one is parsed
-#ifndef PMC_FRONT_PF
-#define PMC_FRONT_PF 0
-#endif
 // (8 waves per SIMD with PMC_FRONT_S10: the packed S leaves room for them at <= 1 KiB; 7 otherwise)
 __global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -74,17 +70,6 @@ __global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kern
             todo &= todo - 1;
             const uint64_t v = g + (uint64_t)jj, gv = a.first + v;
             const uint32_t len = readlane(myl, jj);
-#if PMC_FRONT_PF
-            // L2 prefetch of the grab's next value: one dword per 128-byte line of its bytes, consumed after
-            // this value's parse, so its stage finds them in L2 (as the back kernel does)
-            uint32_t pf = 0;
-            if (todo) {
-                const int j2 = __builtin_ctzll(todo);
-                const uintptr_t sa = (uintptr_t)(a.src + a.src_off[a.first + g + (uint64_t)j2]);
-                const uint32_t ns = (uint32_t)(((sa & 127) + readlane(myl, j2) + 127) >> 7);
-                if ((uint32_t)l < ns) pf = *(PMC_GLB const uint32_t *)((sa & ~(uintptr_t)127) + 128ull * (uint32_t)l);
-            }
-#endif
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
 #ifdef PMC_FAULT_LANE_ORDER // (odd values fail the sort's guard; the even ones reach the back's code-rank guard)
             w.fault_rev = (uint32_t)(gv & 1);
@@ -98,9 +83,6 @@ __global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kern
                 }
                 continue;
             }
-#if PMC_FRONT_PF
-            asm volatile("" ::"v"(pf));
-#endif
             // histograms -> column v of the chunk's interleaved u16 table
             uint32_t nz = 0;
             for (int s = l; s < kLCodes + kDCodes; s += 64) {
