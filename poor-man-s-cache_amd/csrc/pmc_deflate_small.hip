@@ -338,10 +338,6 @@ struct TreeOut {
 #ifndef PMC_SORT_AGG
 #define PMC_SORT_AGG 0
 #endif
-// PMC_SORT_PAIR: (with PMC_SORT_U32) adjacent lanes with the same digit share one sort atomic
-#ifndef PMC_SORT_PAIR
-#define PMC_SORT_PAIR 0
-#endif
 // PMC_SORT_U32: the hash sort's digit counters one u32 per digit (sort_positions2_body)
 #ifndef PMC_SORT_U32
 #define PMC_SORT_U32 1
@@ -532,18 +528,6 @@ struct SmallWave {
                 if (valid && (!inm || l == lead)) old = lds_add(&ctr[d], inm ? (uint32_t)__builtin_popcountll(m) : 1u);
                 const uint32_t base = readlane(old, (int)lead);
                 return inm ? base + (uint32_t)__builtin_popcountll(m & below) : old;
-#elif PMC_SORT_PAIR
-                // adjacent lanes (2i, 2i + 1) with the same digit take one atomic (the even lane adds 2, the odd
-                // lane's slot is the even lane's + 1): runs of one digit serialise half as long, in vector
-                // instructions only (a DPP pair swap), and the slots stay in lane order
-                const uint32_t odd = l & 1u;
-                const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)d, 0xB1, 0xf, 0xf, false);
-                const uint32_t vn = (uint32_t)__builtin_amdgcn_mov_dpp(valid ? 1 : 0, 0xB1, 0xf, 0xf, false);
-                const bool same = valid && vn != 0u && dn == d;
-                uint32_t old = 0;
-                if (valid && !(odd && same)) old = lds_add(&ctr[d], !odd && same ? 2u : 1u);
-                const uint32_t on = (uint32_t)__builtin_amdgcn_mov_dpp((int)old, 0xB1, 0xf, 0xf, false);
-                return odd && same ? on + 1u : old;
 #else
                 return valid ? lds_add(&ctr[d], 1u) : 0u;
 #endif
