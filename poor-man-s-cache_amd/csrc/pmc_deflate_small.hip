@@ -330,10 +330,6 @@ struct TreeOut {
 #else
 #define PMC_NOINLINE_FRONT __noinline__
 #endif
-// PMC_EVAL_OWNLOOP: each eval lane's owner position by a scalar loop, not an LDS mark store/load + max-scan
-#ifndef PMC_EVAL_OWNLOOP
-#define PMC_EVAL_OWNLOOP 0
-#endif
 // PMC_HC_BALLOT: build_cn writes the has-candidate bits by a ballot pass over the counts, not lds_or
 #ifndef PMC_HC_BALLOT
 #define PMC_HC_BALLOT 0
@@ -1128,17 +1124,6 @@ struct SmallWave {
 #endif
         // first lane of each evaluated offset j: offs << 26 | (j + 1) << 19 | fx << 18 | R (offs
         // grows with j, so a max-scan hands every lane its owner); other lanes store to dummy slots
-#if PMC_EVAL_OWNLOOP
-        // (each lane's owner by a scalar loop over the lane-owning offsets, ascending: no LDS round trip)
-        const uint32_t mark = offs << 26 | (l + 1) << 19 | fx << 18 | rx;
-        EV[l] = 0;
-        uint32_t sc = 0;
-        for (uint64_t mm = iml; mm; mm &= mm - 1) {
-            const uint32_t mj = readlane(mark, (int)__builtin_ctzll(mm));
-            sc = l >= (mj >> 26) ? mj : sc;
-        }
-        const bool v = l < nl;
-#else
         PMC_LDS uint32_t *dmy = EV + 64; // (the u8 mark area, 16 words)
         EV[l] = 0;
         (inc ? EV : dmy)[inc ? offs : (l & 15)] = offs << 26 | (l + 1) << 19 | fx << 18 | rx;
@@ -1152,7 +1137,6 @@ struct SmallWave {
 #endif
         const bool v = l < nl;
         const uint32_t sc = wave_incl_max_dpp(mk);
-#endif
         const uint32_t own = v ? ((sc >> 19) & 127) - 1 : 0u;
         const uint32_t P = p0 + own, d = l - (sc >> 26) + 1 + ((sc >> 18) & 1u);
         const uint32_t rxo = sc & 0xffffu;
