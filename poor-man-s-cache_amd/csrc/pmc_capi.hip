@@ -466,7 +466,7 @@ PMC_API uint32_t pmc_gzip_isize(const void *in, size_t in_len) {
 // chain of launches (front, order sort, trees, back; record / lane kernels, CRC verify), which only
 // pays once a batch fills the CUs.
 constexpr uint32_t kLatencyBatch = 64;
-constexpr uint64_t kLatencyMaxLen = 1024;
+constexpr uint64_t kLatencyMaxLen = 4096;
 
 // ---- large values (pmc_deflate_large.hip) ------------------------------------------------------------
 // The batch's values of lo < len <= hi.  Their lengths live on the device: one small readback (a count,
@@ -1111,7 +1111,11 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     // (values of at most kLatencyMaxLen bytes: at 4 KiB the one-kernel paths measured far slower than the
     // throughput pipeline even for a few values -- 64 x 4 KiB compress 35 ms against 1.7 ms, decompress
     // 12.4 ms against 0.9 ms, round 4)
-    const bool latency = n <= kLatencyBatch && max_len <= kLatencyMaxLen;
+    static const uint64_t lat_max = getenv("PMC_LATENCY_MAX_LEN") ? (uint64_t)atoll(getenv("PMC_LATENCY_MAX_LEN"))
+                                                                 : kLatencyMaxLen;
+    static const uint64_t lat_batch = getenv("PMC_LATENCY_BATCH") ? (uint64_t)atoll(getenv("PMC_LATENCY_BATCH"))
+                                                                  : kLatencyBatch;
+    const bool latency = n <= lat_batch && max_len <= lat_max;
     // The latency path's kernel reads its inputs from, and writes its outputs to, coherent host memory in
     // place: no H2D / D2H copies (each a runtime copy kernel of its own) around its one launch.
     const bool zc = latency;

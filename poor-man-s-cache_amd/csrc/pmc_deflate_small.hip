@@ -2682,10 +2682,15 @@ __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
 #ifdef PMC_STAMPS
     w.t_last = __builtin_amdgcn_s_memtime();
 #endif
-    for (uint64_t g = wave * 64; g < a.n; g += nwaves * 64) {
+    // groups of G consecutive values per wave (G = 64 once the batch fills every wave 64 times; a batch
+    // of few values, the latency path's, gets one value per wave instead of all on wave 0 -- 16 x 4 KiB
+    // measured 8.7 ms serialised against 0.54 ms for one)
+    const uint64_t G = min((uint64_t)64, (a.n + nwaves - 1) / nwaves);
+    for (uint64_t g = wave * G; g < a.n; g += nwaves * G) {
         const uint64_t vl = g + (uint64_t)l;
-        const uint32_t myl = vl < a.n ? a.src_len[vl] : 0u;
-        uint64_t todo = ballot(vl < a.n && myl <= a.lds_max_len);
+        const bool in = (uint64_t)l < G && vl < a.n;
+        const uint32_t myl = in ? a.src_len[vl] : 0u;
+        uint64_t todo = ballot(in && myl <= a.lds_max_len);
         while (todo) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;

@@ -1117,16 +1117,19 @@ __global__ void __launch_bounds__(256, 5) inflate_kernel(InflateArgs a) {
 #ifdef PMC_STAMPS
     Wh.t_last = Wl.t_last = __builtin_amdgcn_s_memtime();
 #endif
-    // groups of 64 members per wave; this variant's members picked out by ballot
-    for (uint64_t g = wave * 64; g < a.n; g += nwaves * 64) {
+    // groups of G members per wave (G = 64 once the batch fills every wave 64 times; a few members, the
+    // latency path's, one per wave); this variant's members picked out by ballot
+    const uint64_t G = min((uint64_t)64, (a.n + nwaves - 1) / nwaves);
+    for (uint64_t g = wave * G; g < a.n; g += nwaves * G) {
         const uint64_t vl = g + (uint64_t)l;
+        const bool in = (uint64_t)l < G && vl < a.n;
         uint32_t my_in = 0, my_cap = 0;
-        if (vl < a.n) {
+        if (in) {
             my_in = a.src_len[vl];
             my_cap = a.dst_cap[vl];
         }
         const bool my_fits = my_cap <= a.lds_max_out && my_in <= a.lds_max_in;
-        const bool mine = vl < a.n && (!a.retry_only || a.rc[vl] == kInflateRetry);
+        const bool mine = in && (!a.retry_only || a.rc[vl] == kInflateRetry);
         uint64_t todo = ballot(mine && (kHbm != my_fits));
         while (todo) {
             const int j = __builtin_ctzll(todo);
