@@ -465,7 +465,7 @@ PMC_API uint32_t pmc_gzip_isize(const void *in, size_t in_len) {
 // value (deflate_small_kernel; inflate_kernel for decompress) instead of the throughput pipeline's
 // chain of launches (front, order sort, trees, back; record / lane kernels, CRC verify), which only
 // pays once a batch fills the CUs.
-constexpr uint32_t kLatencyBatch = 64;
+constexpr uint32_t kLatencyBatch = 1024;
 constexpr uint64_t kLatencyMaxLen = 4096;
 
 // ---- large values (pmc_deflate_large.hip) ------------------------------------------------------------
