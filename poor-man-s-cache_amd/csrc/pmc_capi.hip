@@ -1108,9 +1108,8 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     const uint64_t up = al(n * 4ull) * 2 + al(out_bytes + 16);
     // (values above the small kernels' limit keep the throughput path: the wave-per-value kernel
     // that would take them works from HBM and is far slower than the split pipeline's large pass)
-    // (values of at most kLatencyMaxLen bytes: at 4 KiB the one-kernel paths measured far slower than the
-    // throughput pipeline even for a few values -- 64 x 4 KiB compress 35 ms against 1.7 ms, decompress
-    // 12.4 ms against 0.9 ms, round 4)
+    // (limits measured with scripts/few_sweep.py: up to 1,024 values of <= 4 KiB the one-kernel paths beat
+    // the pipeline -- 400 x 4 KiB decompress 0.85 ms against 1.86 ms -- and at 4,096 values they tie)
     static const uint64_t lat_max = getenv("PMC_LATENCY_MAX_LEN") ? (uint64_t)atoll(getenv("PMC_LATENCY_MAX_LEN"))
                                                                  : kLatencyMaxLen;
     static const uint64_t lat_batch = getenv("PMC_LATENCY_BATCH") ? (uint64_t)atoll(getenv("PMC_LATENCY_BATCH"))
