@@ -398,7 +398,36 @@ def batch_bench(args):
             td.append(e0.elapsed_time(e1))
         back = D.Batch(back_dst, boff, blen, n, vlen).host_items()
         bad = int((brc != 0).sum()) + sum(1 for v, w in zip(vals, back) if v != w)
-        # host-resident batches (what the server hook calls), wall clock
+        # host-resident batches through the C-ABI alone (what the server's C++ hook calls: caller arrays
+        # prepared once, pmc_gzip_*_batch_host timed), wall clock
+        import ctypes
+        hsrc = b"".join(vals)
+        hoff = np.arange(n, dtype=np.uint64) * vlen
+        hlen = np.full(n, vlen, dtype=np.uint32)
+        hcap = np.full(n, pmc_codec.gzip_bound(vlen), dtype=np.uint32)
+        hdoff = np.concatenate([[0], np.cumsum(hcap[:-1], dtype=np.uint64)]).astype(np.uint64)
+        hdst = np.empty(int(hcap.sum()) + 16, dtype=np.uint8)
+        hdlen = np.zeros(n, dtype=np.uint32)
+        hrc = np.zeros(n, dtype=np.int32)
+        p = lambda a: a.ctypes.data  # noqa: E731
+        ac, ad = [], []
+        for r in range(reps):
+            t0 = time.perf_counter()
+            assert L.pmc_gzip_compress_batch_host(ctx.handle, hsrc, p(hoff), p(hlen), n, p(hdst), p(hdoff), p(hcap),
+                                                  p(hdlen), p(hrc)) == 0
+            ac.append((time.perf_counter() - t0) * 1e3)
+        bad += int((hrc != 0).sum()) + sum(1 for i in range(n) if hdst[hdoff[i]:hdoff[i] + hdlen[i]].tobytes()
+                                           != members[i])
+        msrc = hdst.tobytes()
+        mlen = hdlen.copy()
+        bdst = np.empty(n * vlen + 16, dtype=np.uint8)
+        for r in range(reps):
+            t0 = time.perf_counter()
+            assert L.pmc_gzip_decompress_batch_host(ctx.handle, msrc, p(hdoff), p(mlen), n, p(bdst), p(hoff), p(hlen),
+                                                    p(hdlen), p(hrc)) == 0
+            ad.append((time.perf_counter() - t0) * 1e3)
+        bad += int((hrc != 0).sum()) + int(bdst[:n * vlen].tobytes() != hsrc)
+        # host-resident batches through the Python mirror (list of bytes in and out), wall clock
         hc, hd = [], []
         for r in range(reps):
             t0 = time.perf_counter()
@@ -414,6 +443,7 @@ def batch_bench(args):
         med = lambda x: float(np.median(x))
         out.append({"values": n, "value_bytes": vlen,
                     "device_ms": {"compress": med(tc), "decompress": med(td)},
+                    "host_abi_ms": {"compress": med(ac), "decompress": med(ad)},
                     "host_ms": {"compress": med(hc), "decompress": med(hd)},
                     "mismatches": bad})
         print(json.dumps(out[-1]), file=sys.stderr, flush=True)
@@ -537,6 +567,9 @@ def main():
                   "ranks_matching": int(p_match), "members": n * world, "method": parity["method"],
                   "reference": parity["reference"]}
 
+    # ---- lane-order guards (DESIGN §4 Guards): over the run, no value may have been rerouted -------
+    guards = ctx.guard_counts()
+
     # ---- per-kernel launch times of one more step (HIP events around every launch) -----------
     ctx.profile(True)
     step()
@@ -621,10 +654,16 @@ def main():
             "ratio": total_comp / total_bytes, "verified_values": int(total_bytes // vlen),
             "mismatches": int(total_bad),
             "fullsize_parity": parity,
+            "guard_counts": guards,
         }
         if h2h:
             out["host_to_host"] = h2h
         print(json.dumps(out), flush=True)
+        # a guard that fired means values silently took the slow retry kernel: fail the run loudly (the
+        # line above still records the counts); large periodic values may legitimately take the stitch's
+        # fallback (guard_counts.retry), small ones never
+        assert guards["sort"] == 0 and guards["codes"] == 0 and guards["probe"] == 0, guards
+        assert vlen > 31808 or guards["retry"] == 0, guards
     if world > 1:
         dist.destroy_process_group()
 

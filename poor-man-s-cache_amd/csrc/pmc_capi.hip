@@ -12,8 +12,10 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
 #include <mutex>
 #include <string>
+#include <thread>
 
 #include "../../include/pmc_codec.h"
 #include "pmc_device.hpp"
@@ -176,7 +178,11 @@ struct pmc_ctx {
     // violations, [3] values sent to the HBM kernel's retry pass by the other paths, [4] members the
     // decompress fast paths handed to the wave kernels; lane_order_ok = the probe passed (else compress takes the kernels that do not need it)
     DevBuf guard;
+    DevBuf rlist;                // compress: the per-call retry list (DeflateArgs::rlist)
     bool lane_order_ok = true;
+    // host-call routing (pmc_ctx_path_counts): [0] / [1] compress / decompress calls on the latency
+    // path, [2] / [3] on the throughput pipeline
+    uint64_t path_calls[4] = {0, 0, 0, 0};
     // large values (pmc_deflate_large.hip): selection list, round tables, round scratch, emit scratch
     DevBuf lvsel, lvtab, lvbuf, lvemit;
     HostBuf lvpin;
@@ -400,6 +406,13 @@ PMC_API int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[5]) {
     return PMC_OK;
 }
 
+PMC_API int pmc_ctx_path_counts(pmc_ctx *ctx, uint64_t counts[4]) {
+    if (!ctx || !counts) return PMC_E_ARG;
+    std::lock_guard<std::mutex> lock(ctx->host_mu);
+    for (int k = 0; k < 4; k++) counts[k] = ctx->path_calls[k];
+    return PMC_OK;
+}
+
 PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -412,6 +425,7 @@ PMC_API void pmc_ctx_destroy(pmc_ctx *c) {
     c->recs.release();
     c->bigl.release();
     c->guard.release();
+    c->rlist.release();
     c->lvsel.release();
     c->lvtab.release();
     c->lvbuf.release();
@@ -661,22 +675,27 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     const bool lv = !force_v1 && max_len > hbm_cut;
     uint64_t hbm_waves = 0, hbm_wb = deflate_wave_bytes(true, max_len);
     // The HBM kernel takes values by length only on the V1 path.  Otherwise it runs gated, as the retry
-    // pass of the values the other paths declined (a lane-order guard fired, a large-pass value of
-    // several blocks, a large value whose segments did not stitch): it returns at once while the
-    // context's counters of those are 0.
+    // pass of the values this call's other paths declined (a lane-order guard fired, a large-pass value
+    // of several blocks, a large value whose segments did not stitch): it visits the call's retry list
+    // (DeflateArgs::rlist) and returns at once when the list is empty.  The latency path launches no
+    // retry pass: host_batch reads the verdicts and redoes a declined call through the pipeline.
     const bool gated = !(force_v1 && max_len > hbm_cut);
-    if (!gated) {
-        // as many waves as the kernel's 196 VGPRs let a CU hold (2 per SIMD) within a 32 GiB scratch
-        // budget: at 2 waves per CU (round 1-2) the latency-bound walk left 64 KiB values at
-        // 0.52 GiB/s
+    if (!gated || !latency) {
+        // as many waves as the kernel's 196 VGPRs let a CU hold (2 per SIMD) within a scratch budget
+        // (32 GiB for the V1 path's length-routed values; 8 GiB for retries, whose waves exit at once
+        // when there are none): at 2 waves per CU (round 1-2) the latency-bound walk left 64 KiB values
+        // at 0.52 GiB/s, and a 64-wave retry pass left periodic 1 MiB values and multi-block 24 KB
+        // values 32x short of that
         hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 8,
-                                                             (32ull << 30) / std::max<uint64_t>(hbm_wb, 1)));
-    } else if (split || lv) {
-        // (the single-kernel path's sort and codes do not use returning-atomic ranks: no retry pass
-        // unless large values ran)
-        hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>(64, (4ull << 30) / std::max<uint64_t>(hbm_wb, 1)));
+                                                             ((gated ? 8ull : 32ull) << 30) / std::max<uint64_t>(hbm_wb, 1)));
     }
     hbm_waves = std::min<uint64_t>(hbm_waves, n);
+    if (gated && hbm_waves) {
+        int r = ctx->rlist.ensure(4ull * ((uint64_t)n + 1));
+        if (r) return r;
+        HIP_TRY(hipMemsetAsync(ctx->rlist.p, 0, 4, st));
+        a.rlist = (uint32_t *)ctx->rlist.p;
+    }
     if (split) {
         // chunk scratch budget (PMC_SPLIT_CHUNK_MB): 96 GiB of the 288 GiB holds 14M 1-KiB values, so the
         // 10M north-star batch is one front/trees/back launch set (~7 KB of chunk arrays per 1 KiB value,
@@ -1086,11 +1105,42 @@ struct HostCall {
     }
 };
 
+// Per-value copies between the caller's buffers and the staging area: one job per value, spread over
+// host threads once a call moves enough bytes that one core's memcpy (~10 GB/s) would show beside the
+// kernels (a 4,096 x 4 KiB batch is 16 MiB in and 17 MiB of slots out).
+template <class F>
+void par_values(uint32_t n, uint64_t bytes, F job) {
+    static const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    static const unsigned cap = getenv("PMC_HOST_THREADS") ? (unsigned)std::max(1, atoi(getenv("PMC_HOST_THREADS")))
+                                                           : std::min(8u, hw);
+    const unsigned t = (unsigned)std::min<uint64_t>({cap, (uint64_t)n, std::max<uint64_t>(1, bytes >> 21)});
+    if (t <= 1) {
+        for (uint32_t i = 0; i < n; i++) job(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(t - 1);
+    auto part = [&](unsigned k) {
+        const uint32_t a = (uint32_t)((uint64_t)n * k / t), b = (uint32_t)((uint64_t)n * (k + 1) / t);
+        for (uint32_t i = a; i < b; i++) job(i);
+    };
+    for (unsigned k = 1; k < t; k++) th.emplace_back(part, k);
+    part(0);
+    for (auto &x : th) x.join();
+}
+
+double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
                uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
                int32_t *rc) {
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
+    static const bool trace = getenv("PMC_HOST_TRACE") && atoi(getenv("PMC_HOST_TRACE"));
+    double t[8] = {};
+    if (trace) t[0] = now_us();
     HostCall guard(ctx);
     HIP_TRY(hipSetDevice(ctx->device));
     // packed device layout, in the order of the two copies: [offsets, lengths, caps | source bytes]
@@ -1106,15 +1156,22 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     auto al = [](uint64_t x) { return (x + 255) & ~(uint64_t)255; };
     const uint64_t down = al(n * 8ull) * 2 + al(n * 4ull) * 2 + al(in_bytes + 16);
     const uint64_t up = al(n * 4ull) * 2 + al(out_bytes + 16);
-    // (values above the small kernels' limit keep the throughput path: the wave-per-value kernel
-    // that would take them works from HBM and is far slower than the split pipeline's large pass)
-    // (limits measured with scripts/few_sweep.py: up to 1,024 values of <= 4 KiB the one-kernel paths beat
-    // the pipeline -- 400 x 4 KiB decompress 0.85 ms against 1.86 ms -- and at 4,096 values they tie)
+    // Routing (limits measured with scripts/few_sweep.py).  Compress: up to 1,024 values of <= 4 KiB the
+    // one-kernel path (deflate_small_kernel) beats the pipeline; above 4 KiB the wave-per-value kernel would
+    // work from HBM, far slower than the split pipeline's large pass.  Decompress: the wave-per-member
+    // inflate kernel holds a member's output in LDS up to inflate_lds_out_limit() (48 KiB), so a member up
+    // to that size stays on the latency path (a 30 KB member: 0.81 ms there against 3.8 ms through the
+    // pipeline); the batch limit is the 1,024 x 4 KiB = 4 MiB of output where the two
+    // paths were measured to cross.
     static const uint64_t lat_max = getenv("PMC_LATENCY_MAX_LEN") ? (uint64_t)atoll(getenv("PMC_LATENCY_MAX_LEN"))
                                                                  : kLatencyMaxLen;
     static const uint64_t lat_batch = getenv("PMC_LATENCY_BATCH") ? (uint64_t)atoll(getenv("PMC_LATENCY_BATCH"))
                                                                   : kLatencyBatch;
-    const bool latency = n <= lat_batch && max_len <= lat_max;
+    const uint64_t lat_dmax = lat_max ? std::max(lat_max, inflate_lds_out_limit()) : 0;
+    const bool latency = dir == kCompress ? n <= lat_batch && max_len <= lat_max
+                                          : n <= lat_batch && max_len <= lat_dmax &&
+                                                (max_len <= lat_max || out_bytes <= lat_batch * lat_max);
+    ctx->path_calls[(latency ? 0 : 2) + (dir == kCompress ? 0 : 1)]++;
     // The latency path's kernel reads its inputs from, and writes its outputs to, coherent host memory in
     // place: no H2D / D2H copies (each a runtime copy kernel of its own) around its one launch.
     const bool zc = latency;
@@ -1161,46 +1218,76 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     for (uint32_t i = 0; i < n; i++) {
         h_soff[i] = so;
         h_slen[i] = src_len[i];
-        memcpy(h_src + so, src + src_off[i], src_len[i]);
         so += src_len[i];
         h_doff[i] = doff;
         h_dcap[i] = dst_cap[i];
         doff += dst_cap[i];
     }
+    par_values(n, in_bytes, [&](uint32_t i) { memcpy(h_src + h_soff[i], src + src_off[i], src_len[i]); });
+    if (trace) t[1] = now_us();
     hipStream_t st = ctx->stream;
     if (!zc) HIP_TRY(hipMemcpyAsync(dp, hp, down, hipMemcpyHostToDevice, st));
-    {
+    auto run = [&](bool lat) -> int {
         const int d = dir == kCompress ? 0 : 1;
         std::lock_guard<std::recursive_mutex> dir_lock(ctx->dir_mu[d]);
-        r = dir_enter(ctx, d, st);
-        if (!r) {
+        int e = dir_enter(ctx, d, st);
+        if (!e) {
             if (dir == kCompress)
-                r = compress_batch_body(ctx, d_src, d_soff, d_slen, n, d_dst, d_doff, d_dcap, d_dlen, d_rc,
-                                        (uint32_t)max_len, st, latency);
+                e = compress_batch_body(ctx, d_src, d_soff, d_slen, n, d_dst, d_doff, d_dcap, d_dlen, d_rc,
+                                        (uint32_t)max_len, st, lat);
             else  // the wave kernels' HBM variant only for members the LDS image cannot hold
-                r = decompress_batch_body(ctx, d_src, d_soff, d_slen, n, d_dst, d_doff, d_dcap, d_dlen, d_rc,
-                                          (uint32_t)max_len, st, latency,
-                                          !latency || max_len > inflate_lds_limit_out(max_len) ||
+                e = decompress_batch_body(ctx, d_src, d_soff, d_slen, n, d_dst, d_doff, d_dcap, d_dlen, d_rc,
+                                          (uint32_t)max_len, st, lat,
+                                          !lat || max_len > inflate_lds_limit_out(max_len) ||
                                               max_in > gzip_bound(inflate_lds_limit_out(max_len)) + 64);
-            const int r2 = dir_leave(ctx, d, st);
-            if (!r) r = r2;
+            const int e2 = dir_leave(ctx, d, st);
+            if (!e) e = e2;
         }
-    }
+        return e;
+    };
+    r = run(latency);
     if (r) {
         // kernels already queued may still read or write the staging (in zero-copy mode the host
         // buffers themselves), which the next call refills: let them drain before returning
         (void)hipStreamSynchronize(st);
         return r;
     }
+    if (trace) t[2] = now_us();
     if (!zc) HIP_TRY(hipMemcpyAsync(h_dlen, d_dlen, up, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    uint64_t po = 0;
+    if (zc && dir == kCompress) {
+        // the latency path launches no retry pass: a value its kernel declined (a lane-order guard fired)
+        // sends the call through the pipeline, whose gated HBM pass redoes it
+        bool again = false;
+        for (uint32_t i = 0; i < n && !again; i++) again = h_rc[i] == kDeflateRetry;
+        if (again) {
+            if ((r = run(false))) {
+                (void)hipStreamSynchronize(st);
+                return r;
+            }
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+    }
+    if (trace) t[3] = now_us();
+    uint64_t moved = 0;
     for (uint32_t i = 0; i < n; i++) {
-        uint64_t to = dst_off ? dst_off[i] : po;
         rc[i] = h_rc[i];
         dst_len[i] = h_dlen[i];
-        if (h_rc[i] == 0) memcpy(dst + to, h_dst + h_doff[i], h_dlen[i]);
-        po += dst_cap[i];
+        if (h_rc[i] == 0) moved += h_dlen[i];
+    }
+    par_values(n, moved, [&](uint32_t i) {
+        if (h_rc[i] != 0) return;
+        uint64_t to = dst_off ? dst_off[i] : h_doff[i];
+        memcpy(dst + to, h_dst + h_doff[i], h_dlen[i]);
+    });
+    if (trace) {
+        t[4] = now_us();
+        fprintf(stderr,
+                "pmc_host_trace %s n=%u in=%llu out=%llu path=%s stage_us=%.1f enqueue_us=%.1f wait_us=%.1f "
+                "unpack_us=%.1f total_us=%.1f\n",
+                dir == kCompress ? "compress" : "decompress", n, (unsigned long long)in_bytes,
+                (unsigned long long)moved, latency ? "latency" : "pipeline", t[1] - t[0], t[2] - t[1], t[3] - t[2],
+                t[4] - t[3], t[4] - t[0]);
     }
     return PMC_OK;
 }

@@ -598,10 +598,11 @@ struct DeflateWave {
 // kHbm=true : working set in scratch + wave * wave_bytes (HBM); CRC table still in LDS.
 template <bool kHbm>
 __global__ void __launch_bounds__(256) deflate_kernel(DeflateArgs a) {
-    // gated launch (the lane-order guards' retry pass of a batch with nothing else for this
-    // kernel): nothing to do while no guard has ever fired in this context
-    // (guard[3]: large values the stitched path declined)
-    if (a.gate && a.guard[0] == 0 && a.guard[1] == 0 && a.guard[3] == 0) return;
+    // gated launch (the retry pass of the values this call's other paths declined: a lane-order
+    // guard fired, a large-pass value of several blocks, a large value whose segments did not
+    // stitch): it visits the call's retry list only, and returns at once when it is empty
+    const uint32_t nretry = a.gate ? a.rlist[0] : 0u;
+    if (a.gate && nretry == 0) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint32_t *crc_tab = reinterpret_cast<uint32_t *>(lds);
     for (int k = threadIdx.x; k < 256; k += blockDim.x) crc_tab[k] = c_crc_table[k];
@@ -636,6 +637,18 @@ __global__ void __launch_bounds__(256) deflate_kernel(DeflateArgs a) {
     W.sync();
     if (l == 0) W.tr->ltree[kEndBlock].fc = 1;
     W.sync();
+    if (a.gate) {
+        for (uint64_t k = wave; k < nretry; k += nwaves) {
+            const uint64_t v = a.rlist[1 + k];
+            const uint64_t len = a.src_len[v];
+            const int rc = W.run(a.src + a.src_off[v], len, a.dst + a.dst_off[v], a.dst_cap[v], a.dst_len + v);
+            if (l == 0) {
+                a.rc[v] = rc;
+                if (rc) a.dst_len[v] = 0;
+            }
+        }
+        return;
+    }
     // wave w owns groups of 64 consecutive values: w, w + nwaves, ...; the lengths of a
     // group are read with one coalesced load and the values this variant handles are
     // picked out by ballot
@@ -712,7 +725,10 @@ __global__ void __launch_bounds__(256) deflate_lv_emit_kernel(DeflateArgs a, Lar
         if (l == 0) {
             a.rc[v] = rc;
             if (rc) a.dst_len[v] = 0;
-            if (rc == kDeflateRetry) atomicAdd(a.guard + 3, 1u); // (the HBM kernel redoes the value)
+            if (rc == kDeflateRetry) { // (the HBM kernel redoes the value)
+                atomicAdd(a.guard + 3, 1u);
+                retry_push(a, v);
+            }
         }
     }
 }

@@ -2707,7 +2707,10 @@ __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
             if (l == 0) {
                 a.rc[v] = rc;
                 if (rc) a.dst_len[v] = 0;
-                if (rc == kDeflateRetry) atomicAdd(a.guard, 1u);
+                if (rc == kDeflateRetry) {
+                    atomicAdd(a.guard, 1u);
+                    retry_push(a, v);
+                }
             }
         }
     }

@@ -568,7 +568,8 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
             if (ntok >= kNtokRetry) { // several blocks, or the sort's guard fired: the HBM kernel
                 if (l == 0) {
                     a.rc[gv] = kDeflateRetry;
-                    if (ntok == kNtokMultiBlock) atomicAdd(a.guard + 3, 1u); // (opens the gated retry pass)
+                    if (ntok == kNtokMultiBlock) atomicAdd(a.guard + 3, 1u);
+                    retry_push(a, gv);
                 }
                 continue;
             }
@@ -583,7 +584,10 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
             if (l == 0) {
                 a.rc[gv] = rc;
                 if (rc) a.dst_len[gv] = 0;
-                if (rc == kDeflateRetry) atomicAdd(a.guard + 1, 1u); // (the code-rank guard fired)
+                if (rc == kDeflateRetry) { // (the code-rank guard fired)
+                    atomicAdd(a.guard + 1, 1u);
+                    retry_push(a, gv);
+                }
             }
             asm volatile("" ::"v"(pf));
         }

@@ -63,7 +63,17 @@ struct DeflateArgs {
     // it returns at once while both counters are 0.
     uint32_t *guard;
     int32_t gate;
+    // per-call retry list: [0] count, [1 + k] the batch index of the k-th value a path declined
+    // (kDeflateRetry); zeroed at the start of every compress call.  The gated HBM pass visits only
+    // these values and returns at once when there are none (a lifetime counter kept the
+    // pass scanning every later batch of the context).
+    uint32_t *rlist;
 };
+
+// A path declines value v (rc = kDeflateRetry): the gated HBM pass of this call redoes it.
+__device__ inline void retry_push(const DeflateArgs &a, uint64_t v) {
+    if (a.rlist) a.rlist[1 + atomicAdd(a.rlist, 1u)] = (uint32_t)v;
+}
 
 // ---- large values (pmc_deflate_large.hip): values above the split pipeline's large pass ---------------
 // Each value's positions are sorted stably by hash in HBM (S, and the rank array R), then cut into

@@ -253,9 +253,19 @@ void PrimeCompress(const std::vector<std::string_view> &values, pmc_ctx *ctx) {
 namespace {
 // PrimeCompressAsync's job and helper thread (per request thread)
 thread_local std::unique_ptr<CompressJob> g_job;
-thread_local std::thread g_job_thread;
+// joined when its request thread exits between PrimeCompressAsync and PrimeCompressWait (an exception
+// unwinding the thread): a joinable std::thread destroyed unjoined would std::terminate the server.
+// (Destroyed before g_job, which was constructed first: the helper's job outlives it.)
+struct JobThread {
+    std::thread t;
+    ~JobThread() {
+        if (t.joinable()) t.join();
+    }
+};
+thread_local JobThread g_job_thread;
 // A context of its own: host calls of one context run one at a time (pmc_codec.h), and this one runs
-// beside the default context's decompress batch, on its own stream.
+// beside the default context's decompress batch, on its own stream -- on the default context's
+// device, which pmc_default_ctx() fixes at device 0.
 pmc_ctx *compress_ctx() {
     static std::once_flag once;
     static pmc_ctx *c = nullptr;
@@ -272,11 +282,11 @@ void PrimeCompressAsync(const std::vector<std::string_view> &values) {
     if (!job->build(g_prime, values)) return;
     CompressJob *j = job.get();
     g_job = std::move(job);
-    g_job_thread = std::thread([j] { j->run(compress_ctx()); });
+    g_job_thread.t = std::thread([j] { j->run(compress_ctx()); });
 }
 
 void PrimeCompressWait() {
-    if (g_job_thread.joinable()) g_job_thread.join();
+    if (g_job_thread.t.joinable()) g_job_thread.t.join();
     if (g_job) {
         g_job->finish(g_prime);
         g_job.reset();

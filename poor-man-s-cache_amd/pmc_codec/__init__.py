@@ -89,6 +89,7 @@ SIGNATURES = {
     "pmc_ctx_profile": (_c.c_int, [_p, _c.c_int]),
     "pmc_ctx_kernel_times": (_c.c_int, [_p, _c.POINTER(_c.c_double), _c.POINTER(_u32), _c.c_int]),
     "pmc_ctx_guard_counts": (_c.c_int, [_p, _c.POINTER(_u32)]),
+    "pmc_ctx_path_counts": (_c.c_int, [_p, _c.POINTER(_u64)]),
 }
 
 # pmc_ctx_kernel_times kinds (include/pmc_codec.h PMC_K_*)
@@ -187,6 +188,16 @@ class Context:
         if rc != 0:
             raise CodecUnavailable(f"pmc_ctx_guard_counts failed ({rc}): {last_error()}")
         return {"sort": c[0], "codes": c[1], "probe": c[2], "retry": c[3], "inflate_retry": c[4]}
+
+    def path_counts(self):
+        """Host-call routes taken so far {latency_compress, latency_decompress, pipeline_compress,
+        pipeline_decompress} (include/pmc_codec.h pmc_ctx_path_counts)."""
+        c = (_u64 * 4)()
+        rc = lib().pmc_ctx_path_counts(self.handle, c)
+        if rc != 0:
+            raise CodecUnavailable(f"pmc_ctx_path_counts failed ({rc})")
+        return {"latency_compress": c[0], "latency_decompress": c[1], "pipeline_compress": c[2],
+                "pipeline_decompress": c[3]}
 
     def close(self):
         if self.handle:

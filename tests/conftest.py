@@ -43,3 +43,32 @@ class Golden:
 @pytest.fixture(scope="session")
 def golden():
     return Golden()
+
+
+class LargeGolden:
+    """tests/golden/large_golden.json (tests/golden/make_large_golden.py): the reference's member of every
+    value of tests/large_values.py, as SHA-256 + length, keyed by the value's SHA-256."""
+
+    def __init__(self):
+        with open(os.path.join(GOLDEN, "large_golden.json")) as f:
+            doc = json.load(f)
+        self.vectors, self.sets = doc["vectors"], doc["sets"]
+
+    @staticmethod
+    def _sha(b):
+        import hashlib
+        return hashlib.sha256(b).hexdigest()
+
+    def mismatches(self, values, members):
+        """Indices whose member is not the reference's (or whose value has no vector)."""
+        bad = []
+        for k, (v, m) in enumerate(zip(values, members)):
+            want = self.vectors.get(self._sha(v))
+            if want is None or len(m) != want["gz_len"] or self._sha(m) != want["gz_sha256"]:
+                bad.append(k)
+        return bad
+
+
+@pytest.fixture(scope="session")
+def large_golden():
+    return LargeGolden()

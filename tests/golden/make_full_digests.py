@@ -12,8 +12,10 @@ compressed members, lengths from the codec) and reports "bitexact"; tests/test_g
 the 200K prefixes through a multi-chunk compress.
 
 Output (data only): tests/golden/full_digests.json
-Usage: python tests/golden/make_full_digests.py [--threads 8] [--ranks]
+Usage: python tests/golden/make_full_digests.py [--threads 8] [--ranks | --large]
   --ranks: tests/golden/rank_digests.json, the per-rank digests of bench.py --gpus 2/4/8
+  --large: add the large-value bench legs (100K x 30 KB, 40K x 64 KiB, 1000 x 1 MiB JSON slices; values
+           longer than the 82 KB corpus are slices of it tiled, as bench.py makes them) to full_digests.json
 """
 import argparse
 import hashlib
@@ -35,6 +37,40 @@ SETS = [(10_000_000, 1024, 0, 0x5EED), (10_000_000, 256, 0, 0x5EED), (1_000_000,
         (1_000_000, 1024, 1, 0xA1B2)]
 CHECKPOINTS = (4096, 200_000, 1_000_000, 2_000_000, 5_000_000, 10_000_000)
 CHUNK = 250_000
+# the large-value bench legs (bench.py --n N --vlen V): the reference's own fixtures' size (tests/data 5_*, 6_*,
+# 29-30 KB), 64 KiB and 1 MiB
+LARGE_SETS = [(100_000, 30_000, 0, 0x5EED), (40_000, 65_536, 0, 0x5EED), (1_000, 1 << 20, 0, 0x5EED)]
+LARGE_CHECKPOINTS = (1_000, 4_096, 10_000)
+CHUNK_BYTES = 1 << 30
+
+
+def bench_corpus(corpus, vlen):  # = bench.py: values longer than the corpus are slices of it tiled
+    return corpus * (vlen // len(corpus) + 2) if vlen > len(corpus) else corpus
+
+
+def digest_set(corpus, n, vlen, kind, seed, checkpoints, threads):
+    corpus = bench_corpus(corpus, vlen)
+    chunk = max(1, min(CHUNK, CHUNK_BYTES // vlen))
+    h = hashlib.sha256()
+    gz_bytes = 0
+    marks = {}
+    for first in range(0, n, chunk):
+        m = min(chunk, n - first)
+        vals = O.gen_values(corpus, seed, kind, first, m, vlen)
+        lens, crcs = O.ref_member_records(vals, threads)
+        cut = first
+        for c in sorted(checkpoints):  # split the chunk at checkpoints that fall inside it
+            if first < c <= first + m:
+                a, b = cut - first, c - first
+                O.member_records_digest(lens[a:b], crcs[a:b], h)
+                gz_bytes += int(lens[a:b].astype(np.uint64).sum())
+                marks[str(c)] = {"sha256": h.copy().hexdigest(), "gz_bytes": gz_bytes}
+                cut = c
+        a = cut - first
+        O.member_records_digest(lens[a:], crcs[a:], h)
+        gz_bytes += int(lens[a:].astype(np.uint64).sum())
+    marks[str(n)] = {"sha256": h.hexdigest(), "gz_bytes": gz_bytes}
+    return {"n": n, "vlen": vlen, "kind": kind, "seed": seed, "first": 0, "prefixes": marks}
 
 
 # multi-GPU weak scaling (bench.py --gpus N): rank r of N compresses the first RANK_N keys "key"+i whose
@@ -89,7 +125,27 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--ranks", action="store_true", help="only the per-rank digests (rank_digests.json)")
+    ap.add_argument("--large", action="store_true", help="add the large-value bench legs to full_digests.json")
     args = ap.parse_args()
+    if args.large:
+        O.build(ref=True)
+        d = os.path.join(HERE, "data")
+        corpus = b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)) if f.endswith(".json"))
+        path = os.path.join(HERE, "full_digests.json")
+        with open(path) as f:
+            doc = json.load(f)
+        keep = [st for st in doc["sets"] if (st["n"], st["vlen"], st["kind"]) not in
+                {(n, v, k) for n, v, k, _ in LARGE_SETS}]
+        for n, vlen, kind, seed in LARGE_SETS:
+            t0 = time.time()
+            st = digest_set(corpus, n, vlen, kind, seed, LARGE_CHECKPOINTS, args.threads)
+            st["corpus"] = "tiled" if vlen > len(corpus) else "as is"
+            keep.append(st)
+            print(f"{n} x {vlen}: {st['prefixes'][str(n)]['gz_bytes']} B, {time.time() - t0:.1f} s", flush=True)
+        doc["sets"] = keep
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1)
+        return
     if args.ranks:
         O.build(ref=True)
         d = os.path.join(HERE, "data")

@@ -104,3 +104,21 @@ def test_murmur_restatement_matches_reference_hash():
     for i, h in zip(z["index"], z["hash"]):
         k = b"key%d" % int(i)
         assert L.oracle_murmur3_x64_128_h1(k, len(k), 0) == int(h), int(i)
+
+
+def test_oracle_matches_large_reference_vectors(golden, large_golden):
+    """The restatement above 82 KB (window slides, block flushes, stored-block window test, 4 MiB runs)
+    against the reference's own members (tests/golden/large_golden.json, tests/golden/make_large_golden.py):
+    every value of every large set, hashed."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    import large_values
+    sets = large_values.all_sets(golden.corpus)
+    assert set(sets) == set(large_golden.sets)
+    n = 0
+    for name, vals in sets.items():
+        got = [O.compress(v) for v in vals]
+        bad = large_golden.mismatches(vals, got)
+        assert not bad, (name, [len(vals[k]) for k in bad[:5]])
+        n += len(vals)
+    assert n == sum(len(v) for v in large_golden.sets.values())

@@ -143,17 +143,40 @@ def _deadlocked(pid):
     return calls.count("202") >= 3  # (main's latch wait, the metrics thread's timed wait, and the accept thread)
 
 
+# what the reference's connect race can cost one attempt of the harness: the first pipelined batch of a
+# connection (-b 100 commands; the workflow phase sends 3 per key) lost or misparsed, on each of its
+# TEST_POOL_SIZE=4 connections
+RACE_MAX_FAILURES = 3 * 100 * 4
+_zlib_attempts = []  # this session's zlib baseline attempts (the reference as deployed)
+
+
+def _race_shaped(rc, rps):
+    """A failed attempt the connect race explains: the harness stalled (a lost first batch leaves its reader
+    waiting), or every phase failed at most the first batch of each of its connections."""
+    if rc is None:
+        return True
+    fails = []
+    for ln in rps:
+        try:
+            fails.append(int(ln.rsplit("Failures:", 1)[1].split()[0].strip(",;")))
+        except (IndexError, ValueError):
+            return False
+    return len(fails) == 4 and all(f <= RACE_MAX_FAILURES for f in fails)
+
+
 @pytest.mark.parametrize("kind", ["zlib", "dropin", "batch"])
 def test_reference_load_test_passes(kind):
     """tcp_server_test.py -p -b 100 verbatim (BASELINE configs[4]); it exits 1 on any failed request.
-    Each attempt is bounded (60 s, a passing run takes ~3 s); up to three attempts, because the
-    reference's connect race (REF_CONNECT_RACE above) fails ~40 % of runs over any codec.  Three
-    failed attempts xfail with that citation; any failure other than a failed run or a stall (a
-    crash of the server, a harness error) fails the test."""
+    Each attempt is bounded (60 s, a passing run takes ~3 s).  The reference's connect race
+    (REF_CONNECT_RACE above) fails ~40 % of runs over any codec, so a failed attempt is retried -- up to
+    three times for the zlib baseline, five for the codec builds -- but only while it is race-shaped (a
+    stall, or no more failures than the first batch of every connection; ADVICE r4: a codec regression
+    answering wrongly would fail far more).  Anything else fails the test at once, as does a crash of the
+    server or a harness error; only attempts that were all race-shaped xfail, with the citation."""
     if not os.path.exists(HARNESS):
         pytest.skip("the reference's harness is only in the build container")
     seen = []
-    for attempt in range(3):  # (RefServer itself restarts a deadlocked server, REF_SELF_DEADLOCK)
+    for attempt in range(3 if kind == "zlib" else 5):  # (RefServer itself restarts a deadlocked server)
         s = RefServer(kind)
         try:
             env = dict(os.environ, CACHE_HOST="127.0.0.1", CACHE_PORT=str(s.port), TEST_DELAY_SEC="0.05",
@@ -168,12 +191,17 @@ def test_reference_load_test_passes(kind):
             assert s.p.poll() is None, "the reference server died under its own load test"
             s.stop(timeout=10)
         rps = [ln for ln in out.splitlines() if "RPS:" in ln]
-        if rc == 0 and len(rps) == 4 and all("Failures: 0" in ln for ln in rps):
+        ok = rc == 0 and len(rps) == 4 and all("Failures: 0" in ln for ln in rps)
+        if kind == "zlib":
+            _zlib_attempts.append("passed" if ok else "stalled" if rc is None else "failed")
+        if ok:
             print(kind, f"attempt {attempt + 1}", *rps, sep="\n  ")
             return
         assert rc in (None, 1), out[-3000:]  # (None: stalled; 1: the harness counted failed requests)
+        assert _race_shaped(rc, rps), f"{kind}: failures beyond the connect race's reach: {rps}"
         seen.append("stalled" if rc is None else [ln.split("—")[-1].strip() for ln in rps])
-    pytest.xfail(f"{REF_CONNECT_RACE}; 3 attempts: {seen}")
+    pytest.xfail(f"{REF_CONNECT_RACE}; {len(seen)} race-shaped attempts: {seen}; zlib baseline this session: "
+                 f"{_zlib_attempts}")
 
 
 @pytest.mark.parametrize("kind", ["dropin", "batch"])
