@@ -1107,13 +1107,14 @@ struct HostCall {
 
 // Per-value copies between the caller's buffers and the staging area: one job per value, spread over
 // host threads once a call moves enough bytes that one core's memcpy (~10 GB/s) would show beside the
-// kernels (a 4,096 x 4 KiB batch is 16 MiB in and 17 MiB of slots out).
+// kernels (a 4,096 x 4 KiB batch is 16 MiB in and 17 MiB of slots out): one thread per MiB, at most 16
+// (a GPU job's CPU share on the MI355X boxes; PMC_HOST_THREADS overrides).
 template <class F>
 void par_values(uint32_t n, uint64_t bytes, F job) {
     static const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     static const unsigned cap = getenv("PMC_HOST_THREADS") ? (unsigned)std::max(1, atoi(getenv("PMC_HOST_THREADS")))
-                                                           : std::min(8u, hw);
-    const unsigned t = (unsigned)std::min<uint64_t>({cap, (uint64_t)n, std::max<uint64_t>(1, bytes >> 21)});
+                                                           : std::min(16u, hw);
+    const unsigned t = (unsigned)std::min<uint64_t>({cap, (uint64_t)n, std::max<uint64_t>(1, bytes >> 20)});
     if (t <= 1) {
         for (uint32_t i = 0; i < n; i++) job(i);
         return;

@@ -148,6 +148,14 @@ def gzip_bound(n: int) -> int:
     return lib().pmc_gzip_bound(n)
 
 
+def gzip_bounds(lengths):
+    """pmc_gzip_bound of every length (numpy): the same closed form (csrc/pmc_kernels.hpp gzip_bound,
+    = oracle_gzip_bound; tests/test_abi.py checks them equal), without a C call per value."""
+    import numpy as np
+    n = np.asarray(lengths, dtype=np.uint64)
+    return (n + (n >> np.uint64(3)) + np.uint64(6) * (n // np.uint64(16383) + np.uint64(1)) + np.uint64(32)).astype(np.uint32)
+
+
 def decompress_capacity(member: bytes) -> int:
     """Output capacity for one gzip member: its ISIZE trailer, clamped to DEFLATE's
     1032:1 maximum expansion (a larger ISIZE cannot belong to a valid member)."""
@@ -228,34 +236,34 @@ class Context:
             return []
         L = lib()
         src = b"".join(items)
-        src_len = np.array([len(x) for x in items], dtype=np.uint32)
+        src_len = np.fromiter(map(len, items), dtype=np.uint32, count=n)
         src_off = np.zeros(n, dtype=np.uint64)
         src_off[1:] = np.cumsum(src_len[:-1], dtype=np.uint64)
         if compress:
-            cap = np.array([gzip_bound(len(x)) for x in items], dtype=np.uint32)
+            cap = gzip_bounds(src_len)
         elif caps is not None:
             cap = np.asarray(caps, dtype=np.uint32)
         else:
-            cap = np.array([decompress_capacity(x) for x in items], dtype=np.uint32)
+            cap = np.fromiter(map(decompress_capacity, items), dtype=np.uint32, count=n)
         dst_off = np.zeros(n, dtype=np.uint64)
         dst_off[1:] = np.cumsum(cap[:-1], dtype=np.uint64)
-        dst = ctypes.create_string_buffer(int(cap.sum()) + 1)
+        dst = np.empty(int(cap.sum()) + 1, dtype=np.uint8)
         dst_len = np.zeros(n, dtype=np.uint32)
         rc = np.zeros(n, dtype=np.int32)
         fn = L.pmc_gzip_compress_batch_host if compress else L.pmc_gzip_decompress_batch_host
-        r = fn(self.handle, src, src_off.ctypes.data, src_len.ctypes.data, n, dst, dst_off.ctypes.data,
+        r = fn(self.handle, src, src_off.ctypes.data, src_len.ctypes.data, n, dst.ctypes.data, dst_off.ctypes.data,
                cap.ctypes.data, dst_len.ctypes.data, rc.ctypes.data)
         if r != 0:
             raise CodecUnavailable(f"batch call failed {r}: {last_error()}")
-        raw = dst.raw
-        res = [(int(rc[i]), raw[int(dst_off[i]):int(dst_off[i]) + int(dst_len[i])] if rc[i] == 0 else b"")
-               for i in range(n)]
+        mv = memoryview(dst)
+        offs, lens, rcs = dst_off.tolist(), dst_len.tolist(), rc.tolist()
+        res = [(c, mv[o:o + ln].tobytes() if c == 0 else b"") for c, o, ln in zip(rcs, offs, lens)]
         if not compress and caps is None:
             # bytes after a member misstated its size (the reference ignores them,
             # gzip_compressor.cpp:96): PMC_E_CAPACITY carries the decoded size; decode those again
-            again = [i for i in range(n) if rc[i] == E_CAPACITY and int(dst_len[i]) > int(cap[i])]
+            again = [i for i in range(n) if rcs[i] == E_CAPACITY and lens[i] > int(cap[i])]
             if again:
-                redo = self._host_batch([items[i] for i in again], False, [int(dst_len[i]) for i in again])
+                redo = self._host_batch([items[i] for i in again], False, [lens[i] for i in again])
                 for i, r in zip(again, redo):
                     res[i] = r
         return res

@@ -28,8 +28,10 @@ def test_library_exports_every_declared_symbol():
 
 def test_bound_matches_oracle():
     from oracle import pyoracle as O
-    for n in (0, 1, 29, 1024, 16383, 16384, 65536, 10 ** 6):
+    ns = (0, 1, 29, 1024, 16382, 16383, 16384, 65536, 10 ** 6, 2 ** 31)
+    for n in ns:
         assert pmc_codec.gzip_bound(n) == O.bound(n)
+    assert pmc_codec.gzip_bounds(ns).tolist() == [pmc_codec.gzip_bound(n) for n in ns]
 
 
 def test_isize_helper():
