@@ -13,6 +13,8 @@
 #include <cstdio>
 #include <cstring>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -914,14 +916,22 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
         if (!no_rec) {
             const uint32_t rstride =
                 (uint32_t)std::min<uint64_t>(kRecMax, std::max<uint64_t>(64, ((uint64_t)max_len + 63) & ~(uint64_t)63));
+            // the 1 KiB image instance when no member may decode to more (max_len: the largest capacity),
+            // else the 4 KiB one (PMC_REC_OUT1K=0: always)
+#ifndef PMC_REC_OUT1K
+#define PMC_REC_OUT1K 1
+#endif
+            const bool out1k = PMC_REC_OUT1K && max_len <= 1024;
+            const void *rk = out1k ? (const void *)inflate_rec_kernel<1024> : (const void *)inflate_rec_kernel<kRecOutMax>;
+            const uint32_t rlds = rec_lds_bytes(out1k ? 1024 : kRecOutMax);
             // exactly the resident blocks: a block owns its rows for the whole grid-stride loop,
             // and blocks beyond residency would start only when the first ones have finished
-            static int rec_per_cu = 0;
+            static int rec_per_cu_k[2] = {0, 0};
+            int &rec_per_cu = rec_per_cu_k[out1k ? 1 : 0];
             if (!rec_per_cu) {
                 int nb = 0;
-                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)inflate_rec_kernel, 64,
-                                                                 kRecLdsBytes) != hipSuccess || nb < 1)
-                    nb = (int)(kLdsPerCu / kRecLdsBytes);
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rk, 64, rlds) != hipSuccess || nb < 1)
+                    nb = (int)(kLdsPerCu / rlds);
                 rec_per_cu = nb;
             }
             // members per grab: the smallest power of two whose grabs fit the resident blocks once, so a small
@@ -932,7 +942,7 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
             while (G < 64 && ((uint64_t)n + G - 1) / G > slots) G *= 2;
             a.rec_group = G;
             const unsigned rb = (unsigned)std::min<uint64_t>(((uint64_t)n + G - 1) / G, slots);
-            a.rec_max_out = kRecOutMax;
+            a.rec_max_out = out1k ? 1024u : kRecOutMax;
             r = ctx->recs.ensure((uint64_t)rb * 64 * rstride * 4 + 256);
             if (r) return r;
             a.rec_work = (uint32_t *)ctx->recs.p;
@@ -948,7 +958,10 @@ static int decompress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_
             if (const char *e = getenv("PMC_STOP_AFTER")) a.stop_after = atoi(e); // 31 prepare, 32 phase A
 #endif
             klaunch(ctx, PMC_K_INFLATE_REC, st,
-                    [&] { hipLaunchKernelGGL(inflate_rec_kernel, dim3(rb), dim3(64), kRecLdsBytes, st, a); });
+                    [&] {
+                        if (out1k) hipLaunchKernelGGL(inflate_rec_kernel<1024>, dim3(rb), dim3(64), rlds, st, a);
+                        else hipLaunchKernelGGL(inflate_rec_kernel<kRecOutMax>, dim3(rb), dim3(64), rlds, st, a);
+                    });
             a.big_only = 1;
         }
         // members of several blocks exist only above 16383 output bytes (zlib flushes every 16383
@@ -1105,29 +1118,77 @@ struct HostCall {
     }
 };
 
-// Per-value copies between the caller's buffers and the staging area: one job per value, spread over
-// host threads once a call moves enough bytes that one core's memcpy (~10 GB/s) would show beside the
-// kernels (a 4,096 x 4 KiB batch is 16 MiB in and 17 MiB of slots out): one thread per MiB, at most 16
-// (a GPU job's CPU share on the MI355X boxes; PMC_HOST_THREADS overrides).
+// Per-value copies between the caller's buffers and the staging area: one job per value, spread over a
+// small pool of persistent host threads once a call moves enough bytes that one core's memcpy (~10 GB/s)
+// would show beside the kernels (a 4,096 x 4 KiB batch is 16 MiB in and 17 MiB of slots out): one part per
+// MiB, at most 8 parts (PMC_HOST_THREADS overrides).  Threads spawned per call cost more than they saved
+// at 16 parts (unpack 0.43 -> 0.7 ms), so the pool's workers live for the process and wait on a condition.
+class CopyPool {
+  public:
+    static CopyPool &get() {
+        static CopyPool *p = new CopyPool(); // (never destroyed: workers may outlive static destructors)
+        return *p;
+    }
+    unsigned parts() const { return nthreads + 1; }
+    // runs part(k) for k = 0 .. t - 1 (t <= parts()), part 0 on the calling thread
+    template <class F>
+    void run(unsigned t, F part) {
+        if (t <= 1) {
+            part(0u);
+            return;
+        }
+        std::lock_guard<std::mutex> one(run_mu); // (calls from several contexts' threads take turns)
+        std::unique_lock<std::mutex> lk(mu);
+        fn = [&part](unsigned k) { part(k); };
+        want = t - 1;
+        taken = 0;
+        left = t - 1;
+        gen++;
+        cv.notify_all();
+        lk.unlock();
+        part(0u);
+        lk.lock();
+        done.wait(lk, [&] { return left == 0; });
+        fn = nullptr;
+    }
+
+  private:
+    CopyPool() {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const unsigned cap = getenv("PMC_HOST_THREADS") ? (unsigned)std::max(1, atoi(getenv("PMC_HOST_THREADS")))
+                                                        : std::min(8u, hw);
+        nthreads = cap - 1;
+        for (unsigned k = 0; k < nthreads; k++) std::thread([this] { loop(); }).detach();
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return gen != seen && taken < want; });
+            seen = gen;
+            const unsigned k = ++taken; // parts 1 .. want
+            auto f = fn;
+            lk.unlock();
+            f(k);
+            lk.lock();
+            if (--left == 0) done.notify_one();
+        }
+    }
+    std::mutex mu, run_mu;
+    std::condition_variable cv, done;
+    std::function<void(unsigned)> fn;
+    unsigned nthreads = 0, want = 0, taken = 0, left = 0;
+    uint64_t gen = 0;
+};
+
 template <class F>
 void par_values(uint32_t n, uint64_t bytes, F job) {
-    static const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    static const unsigned cap = getenv("PMC_HOST_THREADS") ? (unsigned)std::max(1, atoi(getenv("PMC_HOST_THREADS")))
-                                                           : std::min(16u, hw);
-    const unsigned t = (unsigned)std::min<uint64_t>({cap, (uint64_t)n, std::max<uint64_t>(1, bytes >> 20)});
-    if (t <= 1) {
-        for (uint32_t i = 0; i < n; i++) job(i);
-        return;
-    }
-    std::vector<std::thread> th;
-    th.reserve(t - 1);
-    auto part = [&](unsigned k) {
+    CopyPool &P = CopyPool::get();
+    const unsigned t = (unsigned)std::min<uint64_t>({(uint64_t)P.parts(), (uint64_t)n, std::max<uint64_t>(1, bytes >> 20)});
+    P.run(t, [&](unsigned k) {
         const uint32_t a = (uint32_t)((uint64_t)n * k / t), b = (uint32_t)((uint64_t)n * (k + 1) / t);
         for (uint32_t i = a; i < b; i++) job(i);
-    };
-    for (unsigned k = 1; k < t; k++) th.emplace_back(part, k);
-    part(0);
-    for (auto &x : th) x.join();
+    });
 }
 
 double now_us() {

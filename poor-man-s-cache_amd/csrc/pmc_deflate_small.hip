@@ -343,6 +343,9 @@ struct TreeOut {
 #define PMC_SORT_U32 1
 #endif
 // PMC_LDS_B64: the 16-byte window loads (load16) as three aligned ds_read_b64
+#ifndef PMC_SORT_REG
+#define PMC_SORT_REG 0 // register-resident bitonic sort + ranks for 512 < npos <= 1024 (SmallWave::sort_rank_reg; measured slower)
+#endif
 #ifndef PMC_LDS_B64
 #define PMC_LDS_B64 0
 #endif
@@ -354,6 +357,143 @@ __device__ __forceinline__ uint32_t sflag(uint32_t x) {
     asm volatile("" : "+s"(x));
     return x;
 }
+
+// ---- register-resident sort of a value's positions by hash (SmallWave::sort_rank_reg) -----------------
+// (a function of its own: inlined into the front, its 16 key registers raised the parse loop's spills)
+template <int M>
+__device__ __forceinline__ uint32_t xlane(uint32_t v) { // the value of lane l ^ M, M <= 8
+    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+    else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+    else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
+    else {
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false); // lane l - 4
+        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12C, 0xF, 0xF, false); // lane l + 4
+        return (lane_id() & 4) ? dn : up;
+    }
+}
+template <int P, int K, int J>
+struct Bitonic {
+    // one stage (K, J) of the network, then the rest
+    __device__ static __forceinline__ void run(uint32_t (&x)[P], uint32_t l) {
+        if constexpr (J < P) {
+#pragma unroll
+            for (int r = 0; r < P; r++) {
+                if (r & J) continue;
+                const bool asc = (((uint32_t)P * l + (uint32_t)r) & (uint32_t)K) == 0;
+                const uint32_t a = x[r], b = x[r | J];
+                const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+                x[r] = asc ? lo : hi;
+                x[r | J] = asc ? hi : lo;
+            }
+        } else if constexpr (J / P <= 8) {
+            constexpr int M = J / P;
+            // (K > J >= P: the direction is lane-uniform, (P l) & K; the lower lane keeps the min iff ascending)
+            const bool take_min = ((l & (uint32_t)M) == 0) == ((((uint32_t)P * l) & (uint32_t)K) == 0);
+#pragma unroll
+            for (int r = 0; r < P; r++) {
+                const uint32_t y = xlane<M>(x[r]);
+                const uint32_t lo = x[r] < y ? x[r] : y, hi = x[r] < y ? y : x[r];
+                x[r] = take_min ? lo : hi;
+            }
+        } else {
+            constexpr int M = J / P; // 16 or 32: registers 2t, 2t + 1 swap halves, each lane takes one pair
+            const uint32_t low = l & ~(uint32_t)M;
+            const bool asc = (((uint32_t)P * low) & (uint32_t)K) == 0;
+#pragma unroll
+            for (int t = 0; t < P; t += 2) {
+                auto s = M == 16 ? __builtin_amdgcn_permlane16_swap(x[t], x[t + 1], false, false)
+                                 : __builtin_amdgcn_permlane32_swap(x[t], x[t + 1], false, false);
+                const uint32_t a = s[0], b = s[1];
+                const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+                auto u = M == 16 ? __builtin_amdgcn_permlane16_swap(asc ? lo : hi, asc ? hi : lo, false, false)
+                                 : __builtin_amdgcn_permlane32_swap(asc ? lo : hi, asc ? hi : lo, false, false);
+                x[t] = u[0];
+                x[t + 1] = u[1];
+            }
+        }
+        if constexpr (J > 1) Bitonic<P, K, J / 2>::run(x, l);
+        else if constexpr (K < 64 * P) Bitonic<P, K * 2, K>::run(x, l);
+    }
+};
+template <int P, int PK>
+__device__ __noinline__ uint32_t sort_rank_reg_fn(PMC_LDS const uint32_t *bw, PMC_LDS uint16_t *S, PMC_LDS uint16_t *R,
+                                                  PMC_LDS uint64_t *HC, uint32_t npos_) {
+    static_assert(P == 16 && PK == 6, "ranks of 10 bits, counts in R's top 6 bits");
+    constexpr uint32_t RB = 16 - PK, CMAX = (1u << PK) - 1;
+    const uint32_t npos = rfl(npos_);
+    const uint32_t l = (uint32_t)lane_id(), e0 = (uint32_t)P * l;
+    // keys: bytes P l .. P l + P + 2 are dwords P / 4 l .. P / 4 l + P / 4 (one 16-byte and one 4-byte read)
+    uint32_t w[P / 4 + 1];
+    {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u q = *(PMC_LDS const v4u *)(bw + (P / 4) * l);
+        w[0] = q.x;
+        w[1] = q.y;
+        w[2] = q.z;
+        w[3] = q.w;
+        w[4] = bw[(P / 4) * l + 4];
+    }
+    uint32_t x[P];
+#pragma unroll
+    for (int r = 0; r < P; r++) {
+        const uint32_t b4 = __builtin_amdgcn_alignbyte(w[(r >> 2) + 1], w[r >> 2], (uint32_t)(r & 3));
+        x[r] = e0 + (uint32_t)r < npos ? hash3(b4) << 10 | (e0 + (uint32_t)r) : 0xffffffffu;
+    }
+    // HC words to zero while the network runs (ordered before the lds_or below by the wave_sync)
+    for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
+    Bitonic<P, 2, 1>::run(x, l);
+    // sorted: element e0 + r in x[r].  Position 0's rank; run starts (a new hash) and the chain count
+    // of each entry: the entries before it in its run, less position 0 (zlib's NIL, first of its run)
+    uint32_t kz = 0;
+#pragma unroll
+    for (int r = 0; r < P; r++) kz = (x[r] & 1023u) == 0u && x[r] != 0xffffffffu ? e0 + (uint32_t)r + 1u : kz;
+    const uint32_t k0 = wave_max_dpp(kz) - 1u;
+    uint32_t prev0 = (uint32_t)__shfl_up((int)(x[P - 1] >> 10), 1);
+    prev0 = l == 0 ? 0xffffffffu : prev0;
+    uint32_t last = 0;
+    {
+        uint32_t prev = prev0;
+#pragma unroll
+        for (int r = 0; r < P; r++) {
+            const uint32_t h = x[r] >> 10;
+            last = e0 + (uint32_t)r < npos && h != prev ? e0 + (uint32_t)r : last;
+            prev = h;
+        }
+    }
+    // the run start in force at the lane's first entry: the last start of the lanes below
+    uint32_t carry = (uint32_t)__shfl_up((int)wave_incl_max_dpp(last), 1);
+    carry = l == 0 ? 0u : carry;
+    wave_sync();
+    // S in sorted order (two 16-byte stores per lane while the lane's entries are all real)
+    if (e0 + P <= npos) {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        uint32_t pk[P / 2];
+#pragma unroll
+        for (int r = 0; r < P / 2; r++) pk[r] = (x[2 * r] & 1023u) | (x[2 * r + 1] & 1023u) << 16;
+        *(PMC_LDS v4u *)(S + e0) = v4u{pk[0], pk[1], pk[2], pk[3]};
+        *(PMC_LDS v4u *)(S + e0 + 8) = v4u{pk[4], pk[5], pk[6], pk[7]};
+    } else {
+#pragma unroll
+        for (int r = 0; r < P; r++)
+            if (e0 + (uint32_t)r < npos) S[e0 + r] = (uint16_t)(x[r] & 1023u);
+    }
+    uint32_t rs = carry, prev = prev0;
+#pragma unroll
+    for (int r = 0; r < P; r++) {
+        const uint32_t e = e0 + (uint32_t)r, h = x[r] >> 10;
+        rs = e < npos && h != prev ? e : rs;
+        prev = h;
+        if (e < npos) {
+            const uint32_t p = x[r] & 1023u;
+            const uint32_t cnt = e - rs - (rs == k0 && e > rs ? 1u : 0u);
+            R[p] = (uint16_t)(e | (cnt < CMAX ? cnt : CMAX) << RB);
+            if (cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
+        }
+    }
+    wave_sync();
+    return k0 | 0x80000000u; // (SmallWave::kRanked)
+}
+
 
 struct SmallWave {
     // every working array is LDS-typed (ds_* with 32-bit addresses)
@@ -658,6 +798,25 @@ struct SmallWave {
             wave_sync();
         }
         return k0;
+    }
+
+    // ---- register-resident sort of the positions by hash, with their ranks and chain counts -----------
+    // For 512 < npos <= 64 P: lane l holds the keys hash << 10 | position of positions P l .. P l + P - 1
+    // (~0 past npos) in P registers and a bitonic network sorts the wave's 64 P keys, element e = P l + r
+    // in register r of lane l.  Compare-exchanges between registers of one lane are plain min / max;
+    // between lanes l and l ^ m: m = 1, 2 quad_perm DPP, m = 8 row_ror:8, m = 4 row_ror:4 / row_ror:12
+    // (lane l reads lane l - n of its row under row_ror:n), m = 16, 32 v_permlane16/32_swap, which
+    // bring both keys of a pair into one lane for two registers at once and back.  The key order is
+    // (hash, position): the stable order the radix sort produced, by construction, with no LDS
+    // atomics -- the returning atomics of sort_positions2 serialised on repeated trigrams (~1,900
+    // bank-conflict cycles per 1 KiB value, profiles/r04/front) and needed the lane-order guard.  From
+    // the sorted registers the same pass writes S (2 x 16-byte stores per lane), the ranks with their
+    // packed chain counts R and the has-candidate bits HC, which build_cn made from a second walk over
+    // S.  Returns k0 (position 0's rank) | kRanked.
+    static constexpr uint32_t kRanked = 0x80000000u;
+    template <int P, int PK>
+    __device__ __forceinline__ uint32_t sort_rank_reg(uint32_t npos) {
+        return sort_rank_reg_fn<P, PK>(bw, S, R, HC, npos);
     }
 
     // 8 bytes at p (dword-aligned LDS reads + alignbyte; the value is zero padded)
@@ -1328,7 +1487,8 @@ struct SmallWave {
     __device__ __forceinline__ uint32_t parse_ondemand_body(uint32_t npos_, uint32_t len_, uint32_t k0_) {
         const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
         const uint32_t nw = (npos + 63) >> 6;
-        if (sflag(build_cn<PK>(npos, rfl(k0_)))) return kNtokRetry; // (the sort's lane-order guard)
+        if (!(rfl(k0_) & kRanked)) // (sort_rank_reg built R and HC itself)
+            if (sflag(build_cn<PK>(npos, rfl(k0_)))) return kNtokRetry; // (the sort's lane-order guard)
         stamp(11);
         PMC_STOP(13, 0)
         Group g;
@@ -2452,7 +2612,12 @@ struct SmallWave {
         const uint32_t npos = len >= 3 ? len - 2 : 0;
         uint32_t ntok;
         if (npos) {
+#if PMC_SORT_REG
+            const uint32_t k0 = cnp == 6 && npos > 512 ? sort_rank_reg<16, 6>(npos)
+                                                       : sort_positions2(npos, (PMC_LDS uint32_t *)CN);
+#else
             const uint32_t k0 = sort_positions2(npos, (PMC_LDS uint32_t *)CN);
+#endif
             stamp(1);
             PMC_STOP(12, 0)
             ntok = cnp == 6   ? parse_ondemand<6>(npos, len, k0)

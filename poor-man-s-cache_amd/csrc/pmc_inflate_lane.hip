@@ -39,6 +39,11 @@ struct LaneCols {
     static constexpr int kLit = LIT, kDist = DIST;
     static constexpr int kColLit = 0, kColDist = LIT, kColBaseL = LIT + DIST, kColBaseD = kColBaseL + 15;
     static constexpr int kColWords = kColBaseD + 15;
+    // lane_lengths' pass 1: symbol `sym` of the lit/len (lit) or distance list goes to entry `at`
+    __device__ static __forceinline__ void place(PMC_LDS uint16_t *col, bool lit, uint32_t at, uint32_t sym, uint32_t,
+                                                 PMC_LDS const uint8_t *) {
+        col[((lit ? kColLit : kColDist) + at) * 64] = (uint16_t)sym;
+    }
 };
 typedef LaneCols<kLaneLitCap, kLaneDistCap> LaneColsL; // the lane kernel's lists
 constexpr int kColLit = LaneColsL::kColLit, kColDist = LaneColsL::kColDist, kColBaseL = LaneColsL::kColBaseL;
@@ -348,7 +353,7 @@ __device__ bool lane_lengths(LaneIn &in, const LaneClc &clc, uint32_t nlen, uint
                 } else {
                     const uint32_t at = *c;
                     *c = (uint8_t)(at + 1);
-                    col[((lit ? C::kColLit : C::kColDist) + at) * 64] = (uint16_t)(lit ? k : k - nlit);
+                    C::place(col, lit, at, lit ? k : k - nlit, val, bcol);
                 }
             }
         } else {
@@ -360,9 +365,9 @@ __device__ bool lane_lengths(LaneIn &in, const LaneClc &clc, uint32_t nlen, uint
 }
 
 // A block's header (after its BFINAL bit) and code tables, `in` at the BTYPE bits; false = decline.
-template <class C>
-__device__ __forceinline__ bool lane_block(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
-                           LaneCode<15> &dist, bool &fixed, bool *over, int wide_lit, int wide_dist) {
+template <class C, class LC, class DC>
+__device__ __forceinline__ bool lane_block(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LC &lit,
+                           DC &dist, bool &fixed, bool *over, int wide_lit, int wide_dist) {
     const uint32_t btype = in.bits(2);
     if (btype == 0 || btype == 3) return false;
     fixed = btype == 1;
@@ -437,9 +442,9 @@ __device__ __forceinline__ bool lane_block(LaneIn &in, PMC_LDS uint16_t *col, PM
 // (if given) is set when the only reason is C's list capacity: the lane kernel's lists hold it;
 // *multi (if given) when the member's first block is not its last (the multi-block pass takes it).
 // (wide_lit / wide_dist: the capacity *over tests against)
-template <class C>
-__device__ __forceinline__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LaneCode<15> &lit,
-                             LaneCode<15> &dist, bool &fixed, bool *over = nullptr, int wide_lit = kLaneLitCap,
+template <class C, class LC, class DC>
+__device__ __forceinline__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, PMC_LDS uint8_t *bcol, LC &lit,
+                             DC &dist, bool &fixed, bool *over = nullptr, int wide_lit = kLaneLitCap,
                              int wide_dist = kLaneDistCap, bool *multi = nullptr, uint32_t *last = nullptr) {
     if (in.len < 18) return false;
     if (in.byte_at(0) != 0x1f || in.byte_at(1) != 0x8b || in.byte_at(2) != 8 || in.byte_at(3) != 0) return false;
@@ -450,7 +455,7 @@ __device__ __forceinline__ bool lane_prepare(LaneIn &in, PMC_LDS uint16_t *col, 
         if (multi) *multi = true;
         return false;
     }
-    return lane_block<C>(in, col, bcol, lit, dist, fixed, over, wide_lit, wide_dist);
+    return lane_block<C, LC, DC>(in, col, bcol, lit, dist, fixed, over, wide_lit, wide_dist);
 }
 
 // Output of one lane: the last kRing bytes live in an LDS ring (column layout, dword k of

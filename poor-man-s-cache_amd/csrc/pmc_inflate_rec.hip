@@ -32,8 +32,15 @@
 namespace pmc {
 
 #ifndef PMC_REC_STAGE
-#define PMC_REC_STAGE 8
+#define PMC_REC_STAGE 4 // (8 until round 5: 4 frees 1 KB of LDS per wave)
 #endif
+// input window per lane (dwords, refilled by halves with the next half prefetched into registers):
+// (8 fits a 10th wave per CU at the 1 KiB image but measured no faster than 16: round 5, same box)
+#ifndef PMC_REC_WIN
+#define PMC_REC_WIN 16
+#endif
+constexpr uint32_t kRecWinDw = PMC_REC_WIN, kRecWinHalf = kRecWinDw / 2;
+static_assert(kRecWinDw == 8 || kRecWinDw == 16, "window halves of one or two uint4");
 constexpr uint32_t kRecStage = PMC_REC_STAGE;         // staged records per lane (LDS column)
 constexpr uint32_t kRecFlushAt = 4;                   // a lane with a whole group makes the wave flush
 // (a flush leaves < 4 records pending, one step adds one: the ring never holds more than kRecFlushAt)
@@ -44,44 +51,88 @@ static_assert(kRecFlushAt >= 4 && kRecFlushAt <= kRecStage && kRecStage % 4 == 0
 #ifndef PMC_REC_LIT
 #define PMC_REC_LIT 96
 #endif
+// PMC_REC8: the symbol lists as bytes (u16 before round 5): a literal/length symbol is its low 8 bits
+// plus the rule that in each code length's run of the (length, symbol)-sorted list the literals come
+// first, so one byte per length (the run's first entry >= 256: "split") restores the ninth bit.  The
+// columns shrink from 300 to 195 B per lane: 25.3 -> 18.6 KB of LDS per wave, 6 -> 8 waves per CU for
+// the 1 KiB image (the kernel waits on LDS and memory latency; round 2 measured 5 -> 6 waves as
+// 82 -> 70 ms).
+#ifndef PMC_REC8
+#define PMC_REC8 1
+#endif
+// PMC_REC_OUT1K: a batch whose outputs are all <= 1 KiB (dst_cap) runs the instance whose phase B
+// image holds 1 KiB (phase B's LDS then fits inside phase A's); others the 4 KiB image.
+#ifndef PMC_REC_OUT1K
+#define PMC_REC_OUT1K 1
+#endif
 typedef LaneCols<PMC_REC_LIT, 24> RecCols;
+// byte-column layout per lane: lit/len and distance bases (int16 columns, entry i of lane l at u16 word
+// i * 64 + l), then byte columns (entry i at byte i * 64 + l): lit/len symbols' low bytes, the splits
+// (lengths 1..15), distance symbols
+struct RecCols8 {
+    static constexpr int kLit = PMC_REC_LIT, kDist = 24;
+    static constexpr int kColBaseL = 0, kColBaseD = 15;
+    static constexpr uint32_t kSymL = 30 * 128, kSplit = kSymL + kLit * 64, kSymD = kSplit + 15 * 64;
+    static constexpr uint32_t kBytes = kSymD + kDist * 64;
+    static constexpr int kColWords = (int)((kBytes + 127) / 128); // (u16 words per lane, for the layout below)
+    // lane_lengths' pass 1: the symbol's low byte to entry `at`; reaching 256 (end of block, the first
+    // symbol >= 256, always of nonzero length) the current offsets per length are the splits
+    __device__ static __forceinline__ void place(PMC_LDS uint16_t *col, bool lit, uint32_t at, uint32_t sym,
+                                                 uint32_t len, PMC_LDS const uint8_t *bcol) {
+        const uint32_t l = (uint32_t)lane_id();
+        PMC_LDS uint8_t *b = (PMC_LDS uint8_t *)(col - l) + l;
+        if (lit && sym == 256) {
+#pragma unroll
+            for (uint32_t L = 1; L <= 15; L++)
+                b[kSplit + (L - 1) * 64] = L == len ? (uint8_t)at : bcol[(kBColCntL + L) * 64];
+        }
+        b[(lit ? kSymL : kSymD) + at * 64] = (uint8_t)sym;
+    }
+};
+typedef std::conditional<PMC_REC8 != 0, RecCols8, RecCols>::type RecColsK;
 static_assert((kRecStage & (kRecStage - 1)) == 0, "stage ring: a power of two");
-static_assert(kWinDw == 16, "the window prefetch holds one 8-dword half in two uint4");
-// phase A: code columns | input windows | record stage (the build columns live in the last
-// two, which start only after the tables are built)
-constexpr uint32_t kRecWinOff = (uint32_t)RecCols::kColWords * 64 * 2;
-constexpr uint32_t kRecStageOff = kRecWinOff + kWinDw * 64 * 4;
-constexpr uint32_t kRecLdsBytes = kRecStageOff + kRecStage * 64 * 4;
-static_assert((kBColCl + 19) * 64 <= (kWinDw + kRecStage) * 64 * 4, "build columns: window + stage");
+// phase A: code columns | input windows | record stage (the build columns live from the window on,
+// which starts only after the tables are built)
+constexpr uint32_t kRecWinOff = PMC_REC8 ? RecCols8::kBytes : (uint32_t)RecCols::kColWords * 64 * 2;
+static_assert(kRecWinOff % 16 == 0, "window dwords aligned");
+constexpr uint32_t kRecStageOff = kRecWinOff + kRecWinDw * 64 * 4;
+constexpr uint32_t kRecBColBytes = (kBColCl + 19) * 64;
+constexpr uint32_t kRecALds = kRecWinOff + ((kRecWinDw + kRecStage) * 64 * 4 > kRecBColBytes
+                                                ? (kRecWinDw + kRecStage) * 64 * 4 : kRecBColBytes);
 // phase B: two output images (16 B of head room so dword -1 reads) | src u16 | start bitmap |
 // per record: its match distance, or 0 for literals (whose bytes go straight to the image)
-constexpr uint32_t kBOut0 = 16;
-constexpr uint32_t kBOut1 = kBOut0 + kRecOutMax + 32;
-constexpr uint32_t kBSrc = kBOut1 + kRecOutMax + 32;
-constexpr uint32_t kBBits = kBSrc + 2 * kRecOutMax;
-constexpr uint32_t kBRecD = kBBits + kRecOutMax / 8;
-static_assert(kBRecD + 2 * kRecMax <= kRecLdsBytes, "phase B reuses phase A's LDS");
-static_assert(kRecOutMax % 1024 == 0, "positions resolve 1024 at a time");
+template <uint32_t OUT>
+struct RecB {
+    static constexpr uint32_t kOut0 = 16;
+    static constexpr uint32_t kOut1 = kOut0 + OUT + 32;
+    static constexpr uint32_t kSrc = kOut1 + OUT + 32;
+    static constexpr uint32_t kBits = kSrc + 2 * OUT;
+    static constexpr uint32_t kRecD = kBits + OUT / 8;
+    static constexpr uint32_t kEnd = kRecD + 2 * (OUT < kRecMax ? OUT : kRecMax); // (records <= output bytes)
+    static constexpr uint32_t kLds = kEnd > kRecALds ? kEnd : kRecALds;          // phase B reuses phase A's LDS
+    static_assert(OUT % 1024 == 0, "positions resolve 1024 at a time");
+};
+uint32_t rec_lds_bytes(uint32_t out) { return out == 1024 ? RecB<1024>::kLds : RecB<kRecOutMax>::kLds; }
 
-// LaneWin with the next half loaded into registers one advance ahead
+// LaneWinP with the next half loaded into registers one advance ahead
 struct LaneWinP {
+    static constexpr uint32_t kQ = kRecWinHalf / 4; // uint4 per half
     PMC_LDS uint32_t *w;
     PMC_GLB const uint4 *blk;
     uint32_t nblk, head, wlo, nd;
     uint64_t buf;
     uint32_t n;
-    uint4 pa, pb; // dwords wlo + kWinDw .. + kWinHalf - 1
+    uint4 pf[kQ]; // dwords wlo + kRecWinDw .. + kRecWinHalf - 1
     __device__ uint4 block(uint32_t k) const { return k < nblk ? gload16(blk + k) : make_uint4(0, 0, 0, 0); }
-    __device__ void put_half(uint32_t d0, uint4 x, uint4 y) {
-        const uint32_t s0 = d0 & (kWinDw - 1);
-        w[(s0 + 0) * 64] = x.x;
-        w[(s0 + 1) * 64] = x.y;
-        w[(s0 + 2) * 64] = x.z;
-        w[(s0 + 3) * 64] = x.w;
-        w[(s0 + 4) * 64] = y.x;
-        w[(s0 + 5) * 64] = y.y;
-        w[(s0 + 6) * 64] = y.z;
-        w[(s0 + 7) * 64] = y.w;
+    __device__ void put_half(uint32_t d0, const uint4 *x) {
+        const uint32_t s0 = d0 & (kRecWinDw - 1);
+#pragma unroll
+        for (uint32_t q = 0; q < kQ; q++) {
+            w[(s0 + 4 * q + 0) * 64] = x[q].x;
+            w[(s0 + 4 * q + 1) * 64] = x[q].y;
+            w[(s0 + 4 * q + 2) * 64] = x[q].z;
+            w[(s0 + 4 * q + 3) * 64] = x[q].w;
+        }
     }
     __device__ void start(const LaneIn &in, uint64_t bp, bool live) {
         blk = in.blk;
@@ -89,31 +140,35 @@ struct LaneWinP {
         nblk = live ? (uint32_t)((((uintptr_t)in.p & 15) + in.len + 15) / 16) : 0u;
         const uint64_t a = bp + head;
         nd = (uint32_t)(a >> 5);
-        wlo = nd & ~(kWinHalf - 1);
-        const uint4 x0 = block(wlo / 4), x1 = block(wlo / 4 + 1), y0 = block(wlo / 4 + 2), y1 = block(wlo / 4 + 3);
-        pa = block(wlo / 4 + 4);
-        pb = block(wlo / 4 + 5);
-        put_half(wlo, x0, x1);
-        put_half(wlo + kWinHalf, y0, y1);
+        wlo = nd & ~(kRecWinHalf - 1);
+        uint4 x[kQ], y[kQ];
+#pragma unroll
+        for (uint32_t q = 0; q < kQ; q++) {
+            x[q] = block(wlo / 4 + q);
+            y[q] = block(wlo / 4 + kQ + q);
+            pf[q] = block(wlo / 4 + 2 * kQ + q);
+        }
+        put_half(wlo, x);
+        put_half(wlo + kRecWinHalf, y);
         buf = 0;
         n = 0;
         refill();
         drop((uint32_t)(a & 31));
     }
     __device__ void refill() { // branch-free: the dword is read either way (its slot always exists)
-        const uint32_t x = w[(nd & (kWinDw - 1)) * 64];
+        const uint32_t x = w[(nd & (kRecWinDw - 1)) * 64];
         const uint32_t r = n <= 32 ? 1u : 0u;
         buf |= r ? (uint64_t)x << n : 0ull;
         n += 32 * r;
         nd += r;
     }
-    __device__ bool needs() const { return nd + 4 > wlo + kWinDw; }
+    __device__ bool needs() const { return nd + 4 > wlo + kRecWinDw; }
     __device__ void advance() { // retire the consumed older half: the prefetched half takes its slots
-        if (nd >= wlo + kWinHalf) {
-            put_half(wlo + kWinDw, pa, pb);
-            wlo += kWinHalf;
-            pa = block((wlo + kWinDw) / 4);
-            pb = block((wlo + kWinDw) / 4 + 1);
+        if (nd >= wlo + kRecWinHalf) {
+            put_half(wlo + kRecWinDw, pf);
+            wlo += kRecWinHalf;
+#pragma unroll
+            for (uint32_t q = 0; q < kQ; q++) pf[q] = block((wlo + kRecWinDw) / 4 + q);
         }
     }
     __device__ uint32_t peek(uint32_t k) const { return (uint32_t)buf & ((1u << k) - 1); }
@@ -133,7 +188,33 @@ struct LaneWinP {
 typedef uint32_t rec_v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t rec_olen(uint32_t w) { return (w >> 30) ? (w >> 30) : (w & 0xff) + 3; }
 
+// the lit/len code over byte lists (RecCols8): the split of the code length restores bit 8
+struct LaneCode8 : LaneCode<15, int16_t, uint8_t> {
+    PMC_LDS uint8_t *split;
+    template <class R>
+    __device__ __forceinline__ uint32_t sym_at(const R &in, uint32_t &len) const {
+        const uint32_t x = __builtin_bitreverse32(in.peek(15)) >> 17;
+        const uint32_t L = code_len(x);
+        const int idx = (int)base[(L - 1) * 64] + (int)(x >> (15 - L));
+        const uint32_t sp = split[(L - 1) * 64];
+        len = L;
+        return (uint32_t)sym[idx * 64] + ((uint32_t)idx >= sp ? 256u : 0u);
+    }
+    template <class R>
+    __device__ __forceinline__ uint32_t peek_sym(const R &in, uint32_t &len) const { return sym_at(in, len); }
+    template <class R>
+    __device__ __forceinline__ uint32_t decode(R &in) const {
+        uint32_t L;
+        const uint32_t s = sym_at(in, L);
+        in.drop(L);
+        return s;
+    }
+};
+
+template <uint32_t OUT>
 __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
+    typedef RecB<OUT> B;
+    constexpr uint32_t kRecOutMax = OUT; // (this instance's image; members of more output: the lane kernel)
     extern __shared__ __attribute__((aligned(16))) uint16_t lcol[];
     uint8_t *lds = (uint8_t *)lcol;
     const uint32_t lane = threadIdx.x;
@@ -141,10 +222,10 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
     PMC_LDS uint32_t *winw = to_lds<uint32_t>((uint32_t *)(lds + kRecWinOff) + lane);
     PMC_LDS uint32_t *stg = to_lds<uint32_t>((uint32_t *)(lds + kRecStageOff) + lane);
     PMC_LDS uint8_t *bcol = to_lds<uint8_t>(lds + kRecWinOff + lane);
-    PMC_LDS uint8_t *ob0 = to_lds<uint8_t>(lds + kBOut0), *ob1 = to_lds<uint8_t>(lds + kBOut1);
-    PMC_LDS uint16_t *srcv = to_lds<uint16_t>((uint16_t *)(lds + kBSrc));
-    PMC_LDS uint32_t *bits = to_lds<uint32_t>((uint32_t *)(lds + kBBits));
-    PMC_LDS uint16_t *recd = to_lds<uint16_t>((uint16_t *)(lds + kBRecD));
+    PMC_LDS uint8_t *ob0 = to_lds<uint8_t>(lds + B::kOut0), *ob1 = to_lds<uint8_t>(lds + B::kOut1);
+    PMC_LDS uint16_t *srcv = to_lds<uint16_t>((uint16_t *)(lds + B::kSrc));
+    PMC_LDS uint32_t *bits = to_lds<uint32_t>((uint32_t *)(lds + B::kBits));
+    PMC_LDS uint16_t *recd = to_lds<uint16_t>((uint16_t *)(lds + B::kRecD));
     const uint32_t rstride = a.rec_stride;
     PMC_GLB uint32_t *const rows = (PMC_GLB uint32_t *)a.rec_scratch + (uint64_t)blockIdx.x * 64 * rstride;
     PMC_GLB uint32_t *const row = rows + (uint64_t)lane * rstride;
@@ -186,17 +267,30 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                 else if (isz > a.rec_max_out) st = 4;
             }
         }
+#if PMC_REC8
+        LaneCode8 lit;
+        LaneCode<15, int16_t, uint8_t> dist;
+        {
+            PMC_LDS uint8_t *b8 = (PMC_LDS uint8_t *)(col - lane) + lane;
+            lit.base = (PMC_LDS int16_t *)(col + RecCols8::kColBaseL * 64);
+            lit.sym = b8 + RecCols8::kSymL;
+            lit.split = b8 + RecCols8::kSplit;
+            dist.base = (PMC_LDS int16_t *)(col + RecCols8::kColBaseD * 64);
+            dist.sym = b8 + RecCols8::kSymD;
+        }
+#else
         LaneCode<15> lit, dist;
         lit.base = (PMC_LDS int16_t *)(col + RecCols::kColBaseL * 64);
         lit.sym = col + RecCols::kColLit * 64;
         dist.base = (PMC_LDS int16_t *)(col + RecCols::kColBaseD * 64);
         dist.sym = col + RecCols::kColDist * 64;
+#endif
         bool fixed = false;
 #ifdef PMC_STAMPS
         uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
         bool over = false;
-        if (st == 0 && !lane_prepare<RecCols>(in, col, bcol, lit, dist, fixed, &over, kLaneWideLit, kLaneDistCap))
+        if (st == 0 && !lane_prepare<RecColsK>(in, col, bcol, lit, dist, fixed, &over, kLaneWideLit, kLaneDistCap))
             st = over ? 4u : 2u; // (lists the lane kernels hold: theirs)
 #ifdef PMC_STAMPS
         uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -567,5 +661,8 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
 #endif
     }
 }
+
+template __global__ void inflate_rec_kernel<1024>(InflateArgs);
+template __global__ void inflate_rec_kernel<kRecOutMax>(InflateArgs);
 
 } // namespace pmc

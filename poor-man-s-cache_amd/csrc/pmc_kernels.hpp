@@ -194,7 +194,9 @@ template <bool kHbm>
 __global__ void inflate_kernel(InflateArgs a);
 template <int LIT, bool MB>
 __global__ void inflate_lane_kernel(InflateArgs a);
+template <uint32_t OUT>
 __global__ void inflate_rec_kernel(InflateArgs a);
+uint32_t rec_lds_bytes(uint32_t out); // dynamic LDS of inflate_rec_kernel<out>
 __global__ void inflate_verify_kernel(InflateArgs a);
 __global__ void arg_check_kernel(const uint32_t *src_len, uint64_t n, uint64_t max_len, int32_t *rc,
                                  uint32_t *dst_len);
