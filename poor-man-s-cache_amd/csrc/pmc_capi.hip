@@ -669,7 +669,12 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     uint64_t cap = (lds_cut + 63) & ~(uint64_t)63;
     cap = std::min<uint64_t>(cap, force_v1 ? v1_lim : small_lim);
     // large pass: values in (small_lim, big_hi]
-    const bool big_pass = split && max_len > small_lim && big_lim > small_lim;
+    // The split pipeline's large pass (16382 < len <= ~31.8K through the front at one wave per CU, the
+    // front's working set filling the CU's LDS) is off since round 5: the large-value pipeline compresses
+    // these values 1.8x faster (100K x 30 KB: 1.55 -> 2.84 GiB/s, 500K x 20 KB 1.58 -> 3.07, same box,
+    // profiles/r05/large).  PMC_BIG_PASS=1 restores it.
+    static const bool big_env = getenv("PMC_BIG_PASS") && atoi(getenv("PMC_BIG_PASS"));
+    const bool big_pass = split && big_env && max_len > small_lim && big_lim > small_lim;
     const uint64_t big_hi = big_pass ? std::min<uint64_t>(big_lim, max_len) : 0;
     const uint64_t big_cap = big_pass ? std::min<uint64_t>((big_hi + 63) & ~(uint64_t)63, big_lim) : 0;
     const uint64_t hbm_cut = big_pass ? big_hi : lds_cut; // the HBM kernel takes lengths above this

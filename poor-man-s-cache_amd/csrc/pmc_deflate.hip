@@ -451,7 +451,11 @@ struct DeflateWave {
                 pos += readlane(incl, 63);
                 ntok += take;
                 t += take;
-                if (ntok == kSymsPerBlock) flush(false);
+                // zlib's deflate_slow tallies a value's last literal after its loop, where a full symbol buffer
+                // does not flush (deflate.c: _tr_tally_lit, then FLUSH_BLOCK(s, 1)): when that literal is the
+                // block's 16383rd symbol it ends the final block, not a block of its own before an empty one
+                const bool tail_lit = pos == len && readlane(dist, (int)take - 1) == 0u;
+                if (ntok == kSymsPerBlock && !tail_lit) flush(false);
             }
         }
         flush(true);

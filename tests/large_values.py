@@ -86,6 +86,25 @@ def size_classes(corpus, sizes=CLASS_SIZES):
     return vals
 
 
+def block_edges():
+    """Values whose parse ends exactly on a 16383-symbol block boundary with a literal: zlib's deflate_slow
+    tallies the last literal after its loop, where a full symbol buffer does not flush, so the final
+    block holds 16383 symbols (found by searching the oracle's parses of prefixes of seeded random
+    strings; NUL-free, so the reference makes them).  Plus random bytes around one and two blocks
+    (stored blocks, NULs: libz)."""
+    alnum = np.frombuffer(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789", dtype=np.uint8)
+    hexd = np.frombuffer(b"0123456789abcdef", dtype=np.uint8)
+    cuts = {(0, 0): (16929, 33901), (0, 1): (16884, 33875), (0, 2): (16866, 33916), (0, 3): (16888, 33898),
+            (1, 0): (40512, 40515)}
+    vals = []
+    for (a, seed), ns in cuts.items():
+        big = bytes(np.random.default_rng(77 + seed).choice(alnum if a == 0 else hexd, 52000))
+        vals += [big[:n] for n in ns] + [big[:n + 1] for n in ns] + [big[:n - 1] for n in ns]
+    for s in list(range(16380, 16400, 3)) + [32766, 32767, 32768, 32769]:
+        vals.append(bytes(np.random.default_rng(s).integers(0, 256, s, dtype=np.uint8)))
+    return vals
+
+
 def all_sets(corpus):
     """{set name: [values]} -- every set the reference vectors cover."""
     return {
@@ -96,4 +115,5 @@ def all_sets(corpus):
         "mixed_with_small": mixed_with_small(corpus),
         "multi_megabyte": multi_megabyte(corpus),
         "size_classes": size_classes(corpus),
+        "block_edges": block_edges(),
     }

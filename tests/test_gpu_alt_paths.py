@@ -1,6 +1,7 @@
 """GPU: the codec's alternate paths stay bit-exact.  The C-ABI reads its path switches once per
 process (PMC_DEFLATE_MONO: single-kernel small-value compress; PMC_DEFLATE_V1: the general
-kernels for every size; PMC_INFLATE_WAVE: wave-per-member decode only; PMC_INFLATE_REC=0: the
+kernels for every size; PMC_BIG_PASS=1: the split pipeline's large pass for 16383..31808-byte values
+instead of the large-value pipeline; PMC_INFLATE_WAVE: wave-per-member decode only; PMC_INFLATE_REC=0: the
 lane kernel for members of every size instead of the record kernel; PMC_TREES_ORDER=0 /
 PMC_INFLATE_ORDER=0: lanes in index order), so each switch runs every golden vector through
 compress and decompress in a child process of its own, one after the other."""
@@ -40,7 +41,7 @@ sys.exit(1 if bad else 0)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("switch", ["PMC_DEFLATE_MONO=1", "PMC_DEFLATE_V1=1", "PMC_INFLATE_WAVE=1",
+@pytest.mark.parametrize("switch", ["PMC_DEFLATE_MONO=1", "PMC_DEFLATE_V1=1", "PMC_BIG_PASS=1", "PMC_INFLATE_WAVE=1",
                                     "PMC_INFLATE_REC=0", "PMC_TREES_ORDER=0", "PMC_INFLATE_ORDER=0"])
 def test_alternate_path_goldens(switch):
     k, v = switch.split("=")

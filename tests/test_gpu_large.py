@@ -101,3 +101,9 @@ def test_size_classes_100k_to_4m(ctx, D, golden, large_golden):
     """100 KB, 333 KB, 1 MiB and 4 MiB values of tiled JSON, alnum, `xy...` and `a...` in one
     batch, each member the reference's own (period-1/2 runs may take the stitch's fallback)."""
     _check(ctx, D, LV.size_classes(golden.corpus), large_golden, may_fall_back=True)
+
+
+def test_block_edges(ctx, D, large_golden):
+    """A parse ending exactly on a 16383-symbol boundary with a literal (zlib: no flush for the last literal, the
+    final block holds 16383 symbols), and random bytes around one and two blocks (stored blocks)."""
+    _check(ctx, D, LV.block_edges(), large_golden)
