@@ -365,6 +365,8 @@ PMC_API int pmc_ctx_create(int device, pmc_ctx **out) {
                                 (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)deflate_back_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kLdsPerCu));
+    HIP_TRY(hipFuncSetAttribute((const void *)deflate_trees_kernel<kTreesCap1K>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)deflate_trees_kernel<kTreesCap>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)deflate_trees_kernel<kLCodes>,
@@ -731,8 +733,8 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
         }
         static const bool no_order = getenv("PMC_TREES_ORDER") && !atoi(getenv("PMC_TREES_ORDER"));
         // (the front keeps no CRC table in LDS: its grid is sized for the blocks that really fit)
-        const size_t tl_small = (size_t)(kTreesCap + 1) * 64 * 4 + 36 * 64 * 2;
-        const size_t tl_big = (size_t)(kLCodes + 1) * 64 * 4 + 36 * 64 * 2;
+        const size_t tl_small = (size_t)(kTreesCap + 1) * 64 * 4, tl_1k = (size_t)(kTreesCap1K + 1) * 64 * 4;
+        const size_t tl_big = (size_t)(kLCodes + 1) * 64 * 4;
         // one pass over the batch for the values with lo < len <= hi, working sets sized for pcap
         auto run_pass = [&](uint64_t lo, uint64_t hi, uint64_t pcap) -> int {
             const uint64_t fwb = deflate_front_wave_bytes(pcap), bwb = deflate_back_wave_bytes(pcap);
@@ -796,7 +798,8 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
                     a.cO = ord;
                 }
                 klaunch(ctx, PMC_K_DEFLATE_TREES, st, [&] {
-                    hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap>, dim3(tb), dim3(64), tl_small, st, a);
+                    if (pcap <= 1024) hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap1K>, dim3(tb), dim3(64), tl_1k, st, a);
+                    else hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap>, dim3(tb), dim3(64), tl_small, st, a);
                     hipLaunchKernelGGL(deflate_trees_kernel<kLCodes>, dim3(std::min<unsigned>(tb, (unsigned)ctx->cus)),
                                        dim3(64), tl_big, st, a);
                 });

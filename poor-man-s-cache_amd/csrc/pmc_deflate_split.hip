@@ -106,13 +106,39 @@ __global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kern
 #ifndef PMC_TREES_SKIP
 #define PMC_TREES_SKIP 0
 #endif
+// N u16 counters packed two per VGPR.  Every access goes through unrolled selects on the index, so the
+// array stays in registers (an indexed private array would live in scratch).  Round 5: bl_count and the
+// bit-length frequencies moved here from the lane's LDS column (72 B per lane), which with the 79-entry
+// heap of the <= 1 KiB instance takes the kernel from 6 to 8 waves per CU (LDS-bound; it waits on its
+// heap's dependent LDS round trips).  Per-lane VALU is cheap here: one instruction serves 64 values.
+template <int N>
+struct RegU16 {
+    static constexpr int kW = (N + 1) / 2;
+    uint32_t w[kW];
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int j = 0; j < kW; j++) w[j] = 0;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t i) const {
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < kW; j++) x = (i >> 1) == (uint32_t)j ? w[j] : x;
+        return (x >> ((i & 1u) * 16)) & 0xffffu;
+    }
+    __device__ __forceinline__ void add(uint32_t i, int32_t v) { // (fields never go below 0 in use)
+        const uint32_t d = (uint32_t)v << ((i & 1u) * 16);
+#pragma unroll
+        for (int j = 0; j < kW; j++) w[j] += (i >> 1) == (uint32_t)j ? d : 0u;
+    }
+};
+
 // Packed heap entry, as in the wave kernel: (freq << 5 | depth) << 10 | node, so zlib's
 // smaller(n, m) (freq, then depth, <=) is key(n) <= key(m) with key = entry >> 10.
 template <int CAP>
 struct LaneTrees {
     PMC_LDS uint32_t *hp;  // heap, entry i at hp[i * 64]  (column of this lane)
-    PMC_LDS uint16_t *blc; // bl_count[16]
-    PMC_LDS uint16_t *blf; // bit-length tree frequencies [19]
+    RegU16<kMaxBits + 1> blc; // bl_count[16]
+    RegU16<kBLCodes> blf;     // bit-length tree frequencies [19]
     const uint16_t *hist;  // global, this value's row: hist[sym]
     uint8_t *lens;         // global, this value's row: lens[sym]
     uint32_t *mg;          // global column: merge list, mg[i * 64]
@@ -245,7 +271,7 @@ struct LaneTrees {
         // lengths of internal nodes reuse the heap's column (node elems + i - 1 at slot i)
         const uint32_t K = nm;
         uint32_t overflow = 0;
-        for (int b = 0; b <= kMaxBits; b++) blc[b * 64] = 0;
+        blc.zero();
         setH(K, 0);
         // The merge list is read back 8 merges (16 keys) per batch with the next two batches in flight:
         // one dependent global round trip per merge made this replay the kernel's longest wait.
@@ -281,7 +307,7 @@ struct LaneTrees {
                         setH(x - (uint32_t)elems + 1, bits);
                     } else {
                         lens[row0 + x] = (uint8_t)bits;
-                        blc[bits * 64]++;
+                        blc.add(bits, 1);
                         const uint32_t f = key >> 15;
                         const uint32_t xb = xbits(kind, x);
                         opt += __umul24(f, bits + xb);
@@ -299,16 +325,16 @@ struct LaneTrees {
             int ov = (int)overflow;
             do {
                 int bits = max_length - 1;
-                while (blc[bits * 64] == 0) bits--;
-                blc[bits * 64]--;
-                blc[(bits + 1) * 64] += 2;
-                blc[max_length * 64]--;
+                while (blc.get((uint32_t)bits) == 0) bits--;
+                blc.add((uint32_t)bits, -1);
+                blc.add((uint32_t)bits + 1, 2);
+                blc.add((uint32_t)max_length, -1);
                 ov -= 2;
             } while (ov > 0);
             // leaves in zlib's heap[--h] order from the top: n_1, m_1, n_2, m_2, ...
             uint32_t idx = 0;
             for (int bits = max_length; bits != 0; bits--) {
-                uint32_t n = blc[bits * 64];
+                uint32_t n = blc.get((uint32_t)bits);
                 while (n != 0) {
                     const uint32_t key = mg[idx * 64], x = key & 1023;
                     idx++;
@@ -382,14 +408,14 @@ struct LaneTrees {
                 continue;
             }
             if (count < min_count) {
-                blf[curlen * 64] += count;
+                blf.add((uint32_t)curlen, count);
             } else if (curlen != 0) {
-                if (curlen != prevlen) blf[curlen * 64]++;
-                blf[kRep3_6 * 64]++;
+                if (curlen != prevlen) blf.add((uint32_t)curlen, 1);
+                blf.add(kRep3_6, 1);
             } else if (count <= 10) {
-                blf[kRepz3_10 * 64]++;
+                blf.add(kRepz3_10, 1);
             } else {
-                blf[kRepz11_138 * 64]++;
+                blf.add(kRepz11_138, 1);
             }
             count = 0;
             prevlen = curlen;
@@ -401,14 +427,11 @@ struct LaneTrees {
 };
 
 template <int CAP>
-__device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC_LDS uint32_t *col,
-                            PMC_LDS uint16_t *aux) {
+__device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC_LDS uint32_t *col) {
     const uint32_t len = a.src_len[a.first + v];
     if (len == 0 || len <= a.min_len || len > a.lds_max_len || a.cN[v] >= kNtokRetry) return;
     LaneTrees<CAP> t;
     t.hp = col;
-    t.blc = aux;
-    t.blf = aux + 16 * 64;
     t.hist = a.cH + v * kSplitRows;
     t.lens = a.cL + v * kSplitRows;
     t.mg = a.cG + ((slot >> 6) * kMergeRows) * 64 + (slot & 63); // (by lane slot: coalesced)
@@ -427,8 +450,8 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC
         typedef uint32_t v4u __attribute__((ext_vector_type(4)));
         PMC_GLB const v4u *g4 = (PMC_GLB const v4u *)t.hist;
         static_assert(kLCodes * 2 == 35 * 16 + 12 && kDCodes == 30, "distance row at v4u 35, byte 12");
-        // (stage_row below also fills heap slots 0..79 with the 20 x 16-byte lengths row, and the
-        // column has CAP + 1 slots before the blc / blf region)
+        // (stage_row below also fills heap slots 0..79 with the 20 x 16-byte lengths row: the column has
+        // CAP + 1 >= 80 slots)
         static_assert(CAP >= 79, "heap slots 60..74 hold the staged distance frequencies, 0..79 the lengths row");
         v4u d5[5];
 #pragma unroll
@@ -438,11 +461,11 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC
     }
     auto dhist = [&](int s) -> uint32_t { return (t.hp[(60 + (s >> 1)) * 64] >> (16 * (s & 1))) & 0xffffu; };
     const int d_max = t.build(dhist, kDCodes, kLCodes, 1, kMaxBits, opt, stat);
-    for (int s = 0; s < kBLCodes; s++) t.blf[s * 64] = 0;
+    t.blf.zero();
     t.stage_row();
     t.scan(0, l_max);
     t.scan(kLCodes, d_max);
-    auto bfreq = [&](int s) -> uint32_t { return t.blf[s * 64]; };
+    auto bfreq = [&](int s) -> uint32_t { return t.blf.get((uint32_t)s); };
     t.build(bfreq, kBLCodes, kLCodes + kDCodes, 2, kMaxBLBits, opt, stat);
     // max_blindex from the bit-length code's lengths (row bytes 316..334) loaded at once, not one
     // dependent HBM read per step of the loop
@@ -471,19 +494,19 @@ __global__ void __launch_bounds__(64) deflate_trees_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t tl[];
     const uint32_t l = threadIdx.x;
     PMC_LDS uint32_t *col = to_lds<uint32_t>(tl + l);
-    PMC_LDS uint16_t *aux = to_lds<uint16_t>((uint16_t *)(tl + (CAP + 1) * 64) + l);
     if (CAP != kLCodes) {
         // values in cO order: a wave's lanes get heaps of similar size and finish together; the
         // largest heaps first (blocks start in index order), so the kernel's last waves are short
         const uint64_t vi = (uint64_t)blockIdx.x * 64 + l;
-        if (vi < a.count) trees_value<CAP>(a, a.cO ? (uint64_t)a.cO[a.count - 1 - vi] : vi, vi, col, aux);
+        if (vi < a.count) trees_value<CAP>(a, a.cO ? (uint64_t)a.cO[a.count - 1 - vi] : vi, vi, col);
     } else {
         const uint32_t nd = a.cD[a.count];
         for (uint32_t k = blockIdx.x * 64 + l; k < nd; k += gridDim.x * 64)
-            trees_value<CAP>(a, a.cD[k], a.cD[k], col, aux);
+            trees_value<CAP>(a, a.cD[k], a.cD[k], col);
     }
 }
 template __global__ void deflate_trees_kernel<kTreesCap>(DeflateArgs);
+template __global__ void deflate_trees_kernel<kTreesCap1K>(DeflateArgs);
 template __global__ void deflate_trees_kernel<kLCodes>(DeflateArgs);
 
 // ---- back --------------------------------------------------------------------------------------------

@@ -123,6 +123,12 @@ constexpr uint32_t kPlanDeferred = 0xffffffffu;
 #define PMC_TREES_CAP 84
 #endif
 constexpr int kTreesCap = PMC_TREES_CAP; // lane heap capacity of the first trees pass
+// (chunks of values <= 1 KiB: 79, the smallest heap that holds the staged 320-byte lengths row -- 8 waves per
+// CU; 1 KiB JSON slices use 60 lit/len symbols on average, 79 at the 99th percentile)
+#ifndef PMC_TREES_CAP1K
+#define PMC_TREES_CAP1K 79
+#endif
+constexpr int kTreesCap1K = PMC_TREES_CAP1K;
 
 // bytes of chunk scratch per value of the split pipeline
 __host__ __device__ inline uint64_t split_value_bytes(uint64_t cap) {
