@@ -106,32 +106,10 @@ __global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kern
 #ifndef PMC_TREES_SKIP
 #define PMC_TREES_SKIP 0
 #endif
-// N u16 counters packed two per VGPR.  Every access goes through unrolled selects on the index, so the
-// array stays in registers (an indexed private array would live in scratch).  Round 5: bl_count and the
-// bit-length frequencies moved here from the lane's LDS column (72 B per lane), which with the 79-entry
-// heap of the <= 1 KiB instance takes the kernel from 6 to 8 waves per CU (LDS-bound; it waits on its
-// heap's dependent LDS round trips).  Per-lane VALU is cheap here: one instruction serves 64 values.
-template <int N>
-struct RegU16 {
-    static constexpr int kW = (N + 1) / 2;
-    uint32_t w[kW];
-    __device__ __forceinline__ void zero() {
-#pragma unroll
-        for (int j = 0; j < kW; j++) w[j] = 0;
-    }
-    __device__ __forceinline__ uint32_t get(uint32_t i) const {
-        uint32_t x = 0;
-#pragma unroll
-        for (int j = 0; j < kW; j++) x = (i >> 1) == (uint32_t)j ? w[j] : x;
-        return (x >> ((i & 1u) * 16)) & 0xffffu;
-    }
-    __device__ __forceinline__ void add(uint32_t i, int32_t v) { // (fields never go below 0 in use)
-        const uint32_t d = (uint32_t)v << ((i & 1u) * 16);
-#pragma unroll
-        for (int j = 0; j < kW; j++) w[j] += (i >> 1) == (uint32_t)j ? d : 0u;
-    }
-};
-
+// (RegU16, pmc_device.hpp: round 5 moved bl_count and the bit-length frequencies from the lane's LDS column
+// into registers, which with the 79-entry heap of the <= 1 KiB instance takes the kernel from 6 to 8 waves
+// per CU: it is LDS-bound and waits on its heap's dependent LDS round trips.  Per-lane VALU is cheap here:
+// one instruction serves 64 values.)
 // Packed heap entry, as in the wave kernel: (freq << 5 | depth) << 10 | node, so zlib's
 // smaller(n, m) (freq, then depth, <=) is key(n) <= key(m) with key = entry >> 10.
 template <int CAP>

@@ -173,6 +173,36 @@ __device__ __forceinline__ uint32_t popc_lt(uint64_t mask) {
     return (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
 }
 
+// N u16 counters packed two per VGPR.  Every access goes through unrolled selects on the index, so the
+// array stays in registers (an indexed private array would live in scratch): per-lane tables of the
+// lane-per-value kernels (trees, inflate code tables) without LDS round trips.
+template <int N>
+struct RegU16 {
+    static constexpr int kW = (N + 1) / 2;
+    uint32_t w[kW];
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int j = 0; j < kW; j++) w[j] = 0;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t i) const {
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < kW; j++) x = (i >> 1) == (uint32_t)j ? w[j] : x;
+        return (x >> ((i & 1u) * 16)) & 0xffffu;
+    }
+    __device__ __forceinline__ void add(uint32_t i, int32_t v) { // (fields never go below 0 in use)
+        const uint32_t d = (uint32_t)v << ((i & 1u) * 16);
+#pragma unroll
+        for (int j = 0; j < kW; j++) w[j] += (i >> 1) == (uint32_t)j ? d : 0u;
+    }
+    __device__ __forceinline__ void set(uint32_t i, uint32_t v) {
+        const uint32_t sh = (i & 1u) * 16;
+#pragma unroll
+        for (int j = 0; j < kW; j++)
+            w[j] = (i >> 1) == (uint32_t)j ? (w[j] & ~(0xffffu << sh)) | (v & 0xffffu) << sh : w[j];
+    }
+};
+
 // GF(2) product a*b mod P in the reflected CRC-32 domain (zlib 1.2.12 multmodp).
 __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
     uint32_t p = 0;
