@@ -307,7 +307,7 @@ __device__ __forceinline__ void lv_state(uint32_t *spec, uint32_t *cont, uint32_
     if (!last && p >= e && p - e < kLvOverlap) cont[p - e] = w;
 }
 
-__global__ void __launch_bounds__(256, 3) lv_parse_kernel(LargeArgs a) {
+__global__ void __launch_bounds__(256, 8) lv_parse_kernel(LargeArgs a) {
     const uint32_t l = (uint32_t)lane_id();
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -327,6 +327,9 @@ __global__ void __launch_bounds__(256, 3) lv_parse_kernel(LargeArgs a) {
         const uint32_t e = last ? P.len : s + kLvSeg;
         const uint32_t eo = last ? P.len : (e + kLvOverlap < P.len ? e + kLvOverlap : P.len);
         uint32_t *spec = a.map + sg * 2 * kLvOverlap, *cont = spec + kLvOverlap;
+        // (not unrolled: unrolled, the compiler hoists all 64 store addresses out of the segment loop into
+        // 128 VGPRs, which held this kernel at 168 VGPRs / 3 waves per SIMD until round 5)
+#pragma unroll 1
         for (uint32_t k = l; k < 2 * kLvOverlap; k += 64) spec[k] = 0;
         P.tok = a.tok + a.seg_tok0[sg];
         wave_sync_global();

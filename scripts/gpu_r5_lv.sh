@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 5: lv_parse_kernel at 64 VGPRs / 8 waves per SIMD -- large-value tests, then the 30 KB, 64 KiB and
+# 1 MiB legs.
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+T=${TAG:-r5lv}
+O=gpurun_out/$T
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_large.py \
+    > $O/pytest.txt 2>&1; rc=$?
+tail -3 $O/pytest.txt; [ $rc -eq 0 ] || exit $rc
+for cfg in "100000 30000" "40000 65536" "1000 1048576"; do
+  set -- $cfg
+  timeout -k 10 300 python bench.py --no-cpu-baseline --n $1 --vlen $2 --steps 2 > $O/b_$2.json 2> $O/b_$2.err || exit $?
+  python3 scripts/bench_line.py $O/b_$2.json "b_$2"
+done
