@@ -674,9 +674,14 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     // The split pipeline's large pass (16382 < len <= ~31.8K through the front at one wave per CU, the
     // front's working set filling the CU's LDS) is off since round 5: the large-value pipeline compresses
     // these values 1.8x faster (100K x 30 KB: 1.55 -> 2.84 GiB/s, 500K x 20 KB 1.58 -> 3.07, same box,
-    // profiles/r05/large).  PMC_BIG_PASS=1 restores it.
-    static const bool big_env = getenv("PMC_BIG_PASS") && atoi(getenv("PMC_BIG_PASS"));
-    const bool big_pass = split && big_env && max_len > small_lim && big_lim > small_lim;
+    // profiles/r05/large) -- except in small batches: one wave per value of the large pass finishes a
+    // lone 30 KB value in ~5 ms, the large-value pipeline's two 16 KiB segment parses (global-memory
+    // chains) in ~10 ms, so batches of up to 2 values per CU that hold no value above the large pass's
+    // limit keep it (a batch with longer values runs the large-value pipeline anyway and sends all its
+    // values above small_lim there).  PMC_BIG_PASS=1 / 0 forces it on / off.
+    static const int big_env = getenv("PMC_BIG_PASS") ? atoi(getenv("PMC_BIG_PASS")) : -1;
+    const bool big_pick = big_env >= 0 ? big_env != 0 : n <= 2 * (uint64_t)ctx->cus && max_len <= big_lim;
+    const bool big_pass = split && big_pick && max_len > small_lim && big_lim > small_lim;
     const uint64_t big_hi = big_pass ? std::min<uint64_t>(big_lim, max_len) : 0;
     const uint64_t big_cap = big_pass ? std::min<uint64_t>((big_hi + 63) & ~(uint64_t)63, big_lim) : 0;
     const uint64_t hbm_cut = big_pass ? big_hi : lds_cut; // the HBM kernel takes lengths above this
