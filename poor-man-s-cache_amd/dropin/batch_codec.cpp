@@ -156,6 +156,7 @@ struct PrimeState {
         char *data;  // new[] member (nullptr once handed out)
         size_t size;
         std::string spare;  // the member bytes, kept for a second SET of the same value
+        bool dup;           // the batch holds this value more than once: keep the spare
     };
     std::string cvals;
     std::vector<Comp> comp;
@@ -170,6 +171,7 @@ struct PrimeState {
         size_t len;
         int rc;
         std::string spare;  // the value bytes, kept for a second GET of the same member
+        bool dup;           // the dry run read this member more than once: keep the spare
     };
     std::string dmembers;
     std::vector<Dec> dec;
@@ -236,8 +238,16 @@ struct CompressJob {
             char *d = new char[dst_len[k]];
             memcpy(d, dst.data() + dst_off[k], dst_len[k]);
             const uint32_t idx = (uint32_t)P.comp.size();
-            P.comp.push_back({src_off[k], src_len[k], d, dst_len[k], {}});
-            P.cidx.emplace(fingerprint(P.cvals.data() + src_off[k], src_len[k]), idx);
+            const uint64_t fp = fingerprint(P.cvals.data() + src_off[k], src_len[k]);
+            bool dup = false;  // (an equal value earlier in the batch: both keep their member bytes)
+            auto range = P.cidx.equal_range(fp);
+            for (auto it = range.first; it != range.second; ++it) {
+                auto &c = P.comp[it->second];
+                if (c.len == src_len[k] && memcmp(P.cvals.data() + c.off, P.cvals.data() + src_off[k], c.len) == 0)
+                    c.dup = dup = true;
+            }
+            P.comp.push_back({src_off[k], src_len[k], d, dst_len[k], {}, dup});
+            P.cidx.emplace(fp, idx);
         }
     }
 };
@@ -304,10 +314,14 @@ void PrimeCollected(pmc_ctx *ctx) {
     std::vector<Entry> ents;
     std::vector<uint32_t> which;
     for (const auto &c : P.collected) {
-        if (P.didx.count(c.first)) continue;  // one decode per stored member
+        auto seen = P.didx.find(c.first);
+        if (seen != P.didx.end()) {  // one decode per stored member
+            P.dec[seen->second].dup = true;
+            continue;
+        }
         const uint32_t idx = (uint32_t)P.dec.size();
         P.didx.emplace(c.first, idx);
-        P.dec.push_back({P.dmembers.size(), c.second, nullptr, 0, 0, {}});
+        P.dec.push_back({P.dmembers.size(), c.second, nullptr, 0, 0, {}, false});
         P.dmembers.append(c.first, c.second);
         which.push_back(idx);
     }
@@ -354,8 +368,9 @@ bool TakeCompressed(const char *input, size_t len, CompressResult *out) {
         auto &c = P.comp[it->second];
         if (c.len != len || memcmp(P.cvals.data() + c.off, input, len) != 0) continue;
         char *d = c.data;
+        if (!d && !c.dup) break;  // handed out, and no spare: the single-value path compresses it again
         if (d) {
-            c.spare.assign(d, c.size);
+            if (c.dup) c.spare.assign(d, c.size);
             c.data = nullptr;  // ownership passes to the caller (Entry.value, freed by kvs)
         } else {               // the same value twice in one batch: its own copy of the member
             d = new char[c.size];
@@ -390,12 +405,16 @@ bool TakeDecompressed(const char *input, size_t size, DecompressResult *out) {
         return false;
     }
     char *v = d.data;
+    if (!v && !d.dup) {  // handed out, and no spare (a read the dry run did not see): decompress it again
+        P.stats.decompress_misses++;
+        return false;
+    }
     if (!v) {  // handed out already (a second GET of the key in this batch): a copy of the value
         v = new char[d.len + 1];
         memcpy(v, d.spare.data(), d.len);
         v[d.len] = '\0';
     } else {
-        d.spare.assign(v, d.len);
+        if (d.dup) d.spare.assign(v, d.len);
         d.data = nullptr;  // the caller owns it now (the reference server never frees it)
     }
     *out = {v, OPERATION_SUCCESS};

@@ -23,6 +23,7 @@
 //
 // Nothing here parses in place: the reference's parsers write NULs into the read buffer
 // (server.cpp:300, protocol.cpp:384), and the real parse still has to see the untouched bytes.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -96,9 +97,24 @@ bool compression_enabled() {  // main.cpp:22's ENABLE_COMPRESSION, default true
 
 }  // namespace
 
+namespace {
+// where an iteration's time goes (PMC_PRIME_STATS): the peek, the SET batch, the GET dry run, the GET
+// batch, and the whole iteration (end of one endCodecBatch to the end of the next)
+struct HookTimes {
+    double peek = 0, set = 0, dry = 0, get = 0, iter = 0, set_first = -1, get_first = -1;
+    size_t set_values = 0, get_keys = 0;
+    std::chrono::steady_clock::time_point last{};
+};
+HookTimes g_t;
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace
+
 void CacheServer::primeCodecBatch(const std::vector<int> &fds) {
     static const bool enabled = compression_enabled();
     if (!enabled) return;
+    auto t0 = std::chrono::steady_clock::now();
     std::vector<std::string_view> set_values;
     std::vector<std::string> get_keys;
     for (int fd : fds) {
@@ -124,19 +140,32 @@ void CacheServer::primeCodecBatch(const std::vector<int> &fds) {
     // 1 x MI355X at 1 and 4 KiB, 16 connections: 167K / 79K ops/s against 190K / 78K synchronous, so the
     // overlap is not the default.)
     static const bool async_set = std::getenv("PMC_HOOK_ASYNC") && std::atoi(std::getenv("PMC_HOOK_ASYNC"));
+    g_t.peek += ms_since(t0);
+    g_t.set_values += set_values.size();
+    g_t.get_keys += get_keys.size();
+    t0 = std::chrono::steady_clock::now();
     if (!set_values.empty()) {
         if (async_set) pmc_batch::PrimeCompressAsync(set_values);
         else pmc_batch::PrimeCompress(set_values);
+        if (g_t.set_first < 0) g_t.set_first = ms_since(t0); // (the first call creates the codec context)
     }
+    g_t.set += ms_since(t0);
     if (!get_keys.empty()) {
+        t0 = std::chrono::steady_clock::now();
         pmc_batch::BeginCollect();
         for (const std::string &k : get_keys) {
             const auto hash = hashFunc(k.c_str());
             (void)serverShards[hash % numShards].keyValueStore->get(k.c_str(), hash);
         }
+        g_t.dry += ms_since(t0);
+        t0 = std::chrono::steady_clock::now();
         pmc_batch::PrimeCollected();
+        if (g_t.get_first < 0) g_t.get_first = ms_since(t0);
+        g_t.get += ms_since(t0);
     }
+    t0 = std::chrono::steady_clock::now();
     pmc_batch::PrimeCompressWait();
+    g_t.set += ms_since(t0);
 }
 
 namespace {
@@ -149,9 +178,13 @@ void write_stats() {
     if (FILE *f = std::fopen(path, "w")) {
         std::fprintf(f,
                      "{\"batches\": %zu, \"compress_hits\": %zu, \"compress_misses\": %zu, "
-                     "\"decompress_hits\": %zu, \"decompress_misses\": %zu}\n",
+                     "\"decompress_hits\": %zu, \"decompress_misses\": %zu, \"ms\": {\"peek\": %.1f, "
+                     "\"set_batch\": %.1f, \"get_dry_run\": %.1f, \"get_batch\": %.1f, \"iterations\": %.1f, "
+                     "\"first_set_batch\": %.1f, \"first_get_batch\": %.1f}, "
+                     "\"set_values\": %zu, \"get_keys\": %zu}\n",
                      g_last.batches, g_last.compress_hits, g_last.compress_misses, g_last.decompress_hits,
-                     g_last.decompress_misses);
+                     g_last.decompress_misses, g_t.peek, g_t.set, g_t.dry, g_t.get, g_t.iter, g_t.set_first, g_t.get_first, g_t.set_values,
+                     g_t.get_keys);
         std::fclose(f);
     }
 }
@@ -160,5 +193,15 @@ void write_stats() {
 void CacheServer::endCodecBatch() {
     static const bool registered = std::getenv("PMC_PRIME_STATS") && std::atexit(write_stats) == 0;
     pmc_batch::EndBatch();
+    const auto now = std::chrono::steady_clock::now();
+    if (g_t.last != std::chrono::steady_clock::time_point{}) g_t.iter += ms_since(g_t.last);
+    g_t.last = now;
+    // (also rewritten every 200 ms: a server stopped by a signal never runs its atexit handlers)
+    static std::chrono::steady_clock::time_point written = now;
+    if (registered && ms_since(written) > 200.0) {
+        g_last = pmc_batch::GetPrimeStats();
+        write_stats();
+        written = now;
+    }
     if (registered) g_last = pmc_batch::GetPrimeStats();
 }
