@@ -135,11 +135,11 @@ void CacheServer::primeCodecBatch(const std::vector<int> &fds) {
             }
         }
     }
-    // The SET batch, then the GET side.  (PMC_HOOK_ASYNC=1 runs the SET batch on a helper thread with a
-    // context of its own while this thread does the GET dry run and the decompress batch; measured on
-    // 1 x MI355X at 1 and 4 KiB, 16 connections: 167K / 79K ops/s against 190K / 78K synchronous, so the
-    // overlap is not the default.)
-    static const bool async_set = std::getenv("PMC_HOOK_ASYNC") && std::atoi(std::getenv("PMC_HOOK_ASYNC"));
+    // The SET batch runs on a helper thread with a context of its own while this thread does the GET dry
+    // run and the decompress batch (PMC_HOOK_ASYNC=0: one after the other).  Round 4 measured no gain
+    // (1 / 4 KiB, 16 connections: 167K / 79K ops/s against 190K / 78K); since round 5's leaner priming,
+    // 4 KiB at 16 / 64 connections: 117K / 144K against 104K / 132K synchronous (profiles/r05/server).
+    static const bool async_set = !std::getenv("PMC_HOOK_ASYNC") || std::atoi(std::getenv("PMC_HOOK_ASYNC"));
     g_t.peek += ms_since(t0);
     g_t.set_values += set_values.size();
     g_t.get_keys += get_keys.size();
