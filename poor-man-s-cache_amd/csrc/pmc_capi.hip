@@ -485,6 +485,27 @@ PMC_API uint32_t pmc_gzip_isize(const void *in, size_t in_len) {
 // pays once a batch fills the CUs.
 constexpr uint32_t kLatencyBatch = 1024;
 constexpr uint64_t kLatencyMaxLen = 4096;
+// (PMC_LATENCY_MAX_LEN / PMC_LATENCY_BATCH override them; 0 disables the path)
+static uint64_t latency_max_len() {
+    static const uint64_t v = getenv("PMC_LATENCY_MAX_LEN") ? (uint64_t)atoll(getenv("PMC_LATENCY_MAX_LEN")) : kLatencyMaxLen;
+    return v;
+}
+static uint64_t latency_batch() {
+    static const uint64_t v = getenv("PMC_LATENCY_BATCH") ? (uint64_t)atoll(getenv("PMC_LATENCY_BATCH")) : kLatencyBatch;
+    return v;
+}
+static uint64_t inflate_lds_out_limit();
+// the decompress side's length limit: the wave-per-member inflate kernel's LDS image (48 KiB)
+static uint64_t latency_max_out() {
+    return latency_max_len() ? std::max(latency_max_len(), inflate_lds_out_limit()) : 0;
+}
+// the decompress side's batch limit: 4x the compress side's, with at most 4x the output in all (4,096 x
+// 4 KiB members: 0.81 ms device-resident through the wave kernel against 1.69 ms through the pipeline;
+// compress at 4,096 x 4 KiB is faster through the pipeline, 2.86 against 3.33 ms -- round 5, same box)
+static bool latency_decompress(uint64_t n, uint64_t max_out, uint64_t out_bytes) {
+    const uint64_t lb = 4 * latency_batch(), lm = latency_max_len();
+    return n <= lb && max_out <= latency_max_out() && (max_out <= lm || out_bytes <= lb * lm);
+}
 
 // ---- large values (pmc_deflate_large.hip) ------------------------------------------------------------
 // The batch's values of lo < len <= hi.  Their lengths live on the device: one small readback (a count,
@@ -636,7 +657,7 @@ static int large_values(pmc_ctx *ctx, const DeflateArgs &a, uint64_t lo, uint64_
 static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
                                uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap,
                                uint32_t *dst_len, int32_t *rc, uint32_t max_len, void *stream,
-                               bool latency = false) {
+                               bool latency = false, bool small = false) {
     if (!ctx) return PMC_E_ARG;
     if (n == 0) return PMC_OK;
     if (max_len == 0) max_len = 1;
@@ -661,7 +682,9 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
     static const bool mono_env = getenv("PMC_DEFLATE_MONO") && atoi(getenv("PMC_DEFLATE_MONO"));
     // (a context whose lane-order probe failed compresses through the single-kernel path, whose
     // sort and codes use per-lane counters and ballots instead of returning-atomic ranks)
-    const bool mono = mono_env || latency || !ctx->lane_order_ok;
+    // (small: a device-resident batch within the latency path's limits -- the one-kernel path, as for
+    // host calls, but with the argument check and the retry pass of the device-resident API)
+    const bool mono = mono_env || latency || small || !ctx->lane_order_ok;
     const bool split = !force_v1 && !mono;
     const uint64_t small_lim = force_v1 ? 0 : deflate_small_limit();
     const uint64_t big_lim = split ? deflate_big_limit() : small_lim;
@@ -1052,7 +1075,11 @@ PMC_API int pmc_gzip_compress_batch(pmc_ctx *ctx, const uint8_t *src, const uint
     std::lock_guard<std::recursive_mutex> dir_lock(ctx->dir_mu[0]);
     int r = dir_enter(ctx, 0, st);
     if (r) return r;
-    r = compress_batch_body(ctx, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len, stream);
+    // a server-sized batch of small values (<= 1,024 of <= 4 KiB: the host calls' latency-path limits)
+    // takes the one-kernel path here too (400 x 4 KiB: 2.15 -> ~1 ms, round 5)
+    const bool small = n <= latency_batch() && max_len <= latency_max_len();
+    r = compress_batch_body(ctx, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len, stream, false,
+                            small);
     const int r2 = dir_leave(ctx, 0, st);
     return r ? r : r2;
 }
@@ -1067,7 +1094,13 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
     std::lock_guard<std::recursive_mutex> dir_lock(ctx->dir_mu[1]);
     int r = dir_enter(ctx, 1, st);
     if (r) return r;
-    r = decompress_batch_body(ctx, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len, stream);
+    // a server-sized GET batch (<= 4,096 members, capacities within the wave kernel's LDS image and
+    // <= 16 MiB of output in all, the host calls' limits): the wave-per-member kernel alone (whole-wave
+    // Huffman decode per member instead of one lane's; 400 x 4 KiB: 1.47 -> ~0.5 ms, round 5), then the
+    // HBM variant for anything it declined (the lengths are device-resident)
+    const bool small = latency_decompress(n, max_len, (uint64_t)n * max_len);
+    r = decompress_batch_body(ctx, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len, stream, small,
+                              true);
     const int r2 = dir_leave(ctx, 1, st);
     return r ? r : r2;
 }
@@ -1236,16 +1269,11 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     // work from HBM, far slower than the split pipeline's large pass.  Decompress: the wave-per-member
     // inflate kernel holds a member's output in LDS up to inflate_lds_out_limit() (48 KiB), so a member up
     // to that size stays on the latency path (a 30 KB member: 0.81 ms there against 3.8 ms through the
-    // pipeline); the batch limit is the 1,024 x 4 KiB = 4 MiB of output where the two
-    // paths were measured to cross.
-    static const uint64_t lat_max = getenv("PMC_LATENCY_MAX_LEN") ? (uint64_t)atoll(getenv("PMC_LATENCY_MAX_LEN"))
-                                                                 : kLatencyMaxLen;
-    static const uint64_t lat_batch = getenv("PMC_LATENCY_BATCH") ? (uint64_t)atoll(getenv("PMC_LATENCY_BATCH"))
-                                                                  : kLatencyBatch;
-    const uint64_t lat_dmax = lat_max ? std::max(lat_max, inflate_lds_out_limit()) : 0;
+    // pipeline); its batch limit is 4,096 members / 16 MiB of output (latency_decompress:
+    // round 5 measured the wave kernel still 2x ahead there).
+    const uint64_t lat_max = latency_max_len(), lat_batch = latency_batch();
     const bool latency = dir == kCompress ? n <= lat_batch && max_len <= lat_max
-                                          : n <= lat_batch && max_len <= lat_dmax &&
-                                                (max_len <= lat_max || out_bytes <= lat_batch * lat_max);
+                                          : latency_decompress(n, max_len, out_bytes);
     ctx->path_calls[(latency ? 0 : 2) + (dir == kCompress ? 0 : 1)]++;
     // The latency path's kernel reads its inputs from, and writes its outputs to, coherent host memory in
     // place: no H2D / D2H copies (each a runtime copy kernel of its own) around its one launch.

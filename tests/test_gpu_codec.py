@@ -659,6 +659,40 @@ def test_latency_path_batches_vs_reference(ctx, golden, dig):
     assert after["pipeline_decompress"] == mid["pipeline_decompress"]
 
 
+@pytest.mark.parametrize("dig", [0, 2], ids=["256B", "4KiB"])
+def test_device_small_batches_vs_reference(ctx, D, golden, dig):
+    """Device-resident calls within the latency limits (<= 1,024 values of <= 4 KiB compress, <= 4,096 members
+    decompress) run the one-kernel paths since round 5 (pmc_gzip_*_batch): batches of 1, 64, 400 and 1,024
+    values of a digest set must give the reference's members (SHA-256 over all of them and their sizes),
+    and batches of 1, 1,000 and 4,096 of those members must decode to the values."""
+    from oracle import pyoracle as O
+    d = golden.index["digests"][dig]
+    vals = [v.tobytes() for v in O.gen_values(golden.corpus, d["seed"], d["kind"], 0, d["n"], d["vlen"])]
+    members, k = [], 0
+    for m in [1, 64, 400] + [1024] * 64:
+        if k >= len(vals):
+            break
+        out, rc = D.compress(ctx, D.pack(vals[k:k + m]))
+        sync()
+        assert int((rc != 0).sum()) == 0, (k, m)
+        members += out.host_items()
+        k += m
+    h = hashlib.sha256(b"".join(members)).hexdigest()
+    sizes = hashlib.sha256(np.asarray([len(g) for g in members], np.uint32).tobytes()).hexdigest()
+    assert h == d["sha256"] and sizes == d["sizes_sha256"], "device small-batch members differ from the reference"
+    back, k = [], 0
+    for m in [1, 1000] + [4096] * 64:
+        if k >= len(members):
+            break
+        part = members[k:k + m]
+        out, rc = D.decompress(ctx, D.pack(part), [d["vlen"]] * len(part))
+        sync()
+        assert int((rc != 0).sum()) == 0, (k, m)
+        back += out.host_items()
+        k += m
+    assert back == vals
+
+
 def test_latency_path_decompress_json_fixtures(ctx, golden):
     """The reference's own 29-30 KB fixtures (tests/data, gzip_compressor_test / kvs_test LargeJSONFiles) decode
     one per call and all together on the latency path (members up to the inflate kernel's 48 KiB LDS image;
