@@ -1098,7 +1098,10 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
     // <= 16 MiB of output in all, the host calls' limits): the wave-per-member kernel alone (whole-wave
     // Huffman decode per member instead of one lane's; 400 x 4 KiB: 1.47 -> ~0.5 ms, round 5), then the
     // HBM variant for anything it declined (the lengths are device-resident)
-    const bool small = latency_decompress(n, max_len, (uint64_t)n * max_len);
+    // A batch of at most 4 members per CU also takes the wave kernels whatever its sizes: one wave per
+    // member beats one lane per member until the lanes' density pays (1000 x 1 MiB: 220 ms against 453 ms
+    // through the multi-block lane pass; 40K x 64 KiB: 542 ms against 25 ms -- round 5, same box).
+    const bool small = latency_decompress(n, max_len, (uint64_t)n * max_len) || (uint64_t)n <= 4ull * ctx->cus;
     r = decompress_batch_body(ctx, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len, stream, small,
                               true);
     const int r2 = dir_leave(ctx, 1, st);
