@@ -1487,7 +1487,7 @@ struct SmallWave {
     __device__ __forceinline__ uint32_t parse_ondemand_body(uint32_t npos_, uint32_t len_, uint32_t k0_) {
         const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
         const uint32_t nw = (npos + 63) >> 6;
-        if (!(rfl(k0_) & kRanked)) // (sort_rank_reg built R and HC itself)
+        if (!PMC_SORT_REG || !(rfl(k0_) & kRanked)) // (sort_rank_reg built R and HC itself)
             if (sflag(build_cn<PK>(npos, rfl(k0_)))) return kNtokRetry; // (the sort's lane-order guard)
         stamp(11);
         PMC_STOP(13, 0)
