@@ -828,7 +828,8 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
                 klaunch(ctx, PMC_K_DEFLATE_TREES, st, [&] {
                     if (pcap <= 1024) hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap1K>, dim3(tb), dim3(64), tl_1k, st, a);
                     else hipLaunchKernelGGL(deflate_trees_kernel<kTreesCap>, dim3(tb), dim3(64), tl_small, st, a);
-                    hipLaunchKernelGGL(deflate_trees_kernel<kLCodes>, dim3(std::min<unsigned>(tb, (unsigned)ctx->cus)),
+                    // (the overflow list's walker: its 73.5 KB heap column fits two one-wave blocks per CU)
+                    hipLaunchKernelGGL(deflate_trees_kernel<kLCodes>, dim3(std::min<unsigned>(tb, 2u * (unsigned)ctx->cus)),
                                        dim3(64), tl_big, st, a);
                 });
                 a.wave_bytes = bwb;
