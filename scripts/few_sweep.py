@@ -16,18 +16,16 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "poor-man-s-cache_amd")]
 import numpy as np  # noqa: E402
 
 import pmc_codec  # noqa: E402
-from oracle import pyoracle as O  # noqa: E402
+from values import gen_values  # noqa: E402  (scripts/values.py: the device generator)
 
 
 def main():
-    d = os.path.join(ROOT, "tests", "golden", "data")
-    corpus = b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)) if f.endswith(".json"))
     ctx = pmc_codec.Context(0)
     few = os.environ.get("PMC_LATENCY_MAX_LEN", "default") + "/" + os.environ.get("PMC_LATENCY_BATCH", "default")
     sizes = [int(x) for x in os.environ.get("SWEEP_N", "1,4,16,64").split(",")]
     for vlen in (256, 1024, 4096):
         for n in sizes:
-            vals = [v.tobytes() for v in O.gen_values(corpus, 0x5EED, 0, 0, n, vlen)]
+            vals = gen_values(n, vlen)
             ref = ctx.compress_many(vals)
             assert all(r == 0 for r, _ in ref)
             members = [g for _, g in ref]

@@ -9,8 +9,6 @@ mkdir -p $O
 timeout -k 10 900 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_large.py tests/test_gpu_alt_paths.py \
     tests/test_gpu_guard.py tests/test_gpu_codec.py tests/test_gpu_inflate_rec.py > $O/pytest.txt 2>&1; rc=$?
 tail -3 $O/pytest.txt; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python scripts/lv_probe.py > $O/lv_probe.txt 2>&1 || exit $?
-tail -2 $O/lv_probe.txt
 for cfg in "100000 30000" "40000 65536"; do
   set -- $cfg
   timeout -k 10 300 python bench.py --no-cpu-baseline --n $1 --vlen $2 --steps 2 > $O/b_$2.json 2> $O/b_$2.err || exit $?

@@ -20,6 +20,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "poor-man-s-cache_amd")]
 
 import pmc_codec  # noqa: E402
+from values import gen_values  # noqa: E402  (scripts/values.py: the device generator)
+# (oracle/_ref is loaded only to time the reference codec itself -- this script's CPU baseline, as bench.py's
+# cpu_baseline leg does; every drop-in call measured goes through libpmc_codec)
 from oracle import pyoracle as O  # noqa: E402
 
 
@@ -27,8 +30,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=2000)
     args = ap.parse_args()
-    d = os.path.join(ROOT, "tests", "golden", "data")
-    corpus = b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)) if f.endswith(".json"))
     L = pmc_codec.lib()
     ctx = L.pmc_default_ctx()
     assert ctx, "no device"
@@ -36,7 +37,7 @@ def main():
     out = {"note": __doc__.split("\n\n")[1].replace("\n", " "), "sizes": []}
     for vlen in (32, 256, 1024, 4096, 30000):
         n = args.calls if vlen <= 4096 else max(200, args.calls // 5)
-        vals = [v.tobytes() for v in O.gen_values(corpus, 0x5EED, 0, 0, n, vlen)]
+        vals = gen_values(n, vlen)
         cap = pmc_codec.gzip_bound(vlen)
         obuf = ctypes.create_string_buffer(cap)
         dbuf = ctypes.create_string_buffer(vlen + 64)
