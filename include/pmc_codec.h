@@ -306,10 +306,13 @@ int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[5]);
 /* Host-call routing counters (build-owned; no reference counterpart).  Every host-memory call
  * (pmc_gzip_*_batch_host and the single-value pmc_gzip_compress / pmc_gzip_decompress on top of it)
  * takes one of two routes: the latency path (one wave-per-value kernel reading and writing coherent
- * host memory in place; compress: <= 1,024 values of <= 4 KiB; decompress: <= 1,024 members of
- * <= 48 KiB output, at most 4 MiB in all) or the throughput pipeline (pinned staging, H2D, the
+ * host memory in place; compress: <= 1,024 values of <= 4 KiB; decompress: <= 4,096 members of
+ * <= 48 KiB output, at most 16 MiB in all) or the throughput pipeline (pinned staging, H2D, the
  * kernel pipeline, D2H).  counts[0] / counts[1]: compress / decompress calls on the latency path;
- * counts[2] / counts[3]: on the pipeline.  Host-side, no device synchronization. */
+ * counts[2] / counts[3]: on the pipeline.  Host-side, no device synchronization.  (The
+ * device-resident pmc_gzip_*_batch calls route batches within the same limits -- and decompress
+ * batches of at most 4 members per CU of any size -- to the same one-kernel paths; they are not
+ * counted here.) */
 int pmc_ctx_path_counts(pmc_ctx *ctx, uint64_t counts[4]);
 
 #ifdef __cplusplus
