@@ -1,7 +1,9 @@
 """Host-memory calls of at most 64 values: latency path (one wave-per-value kernel over coherent host memory)
 against the throughput pipeline.  Run twice, PMC_LATENCY_MAX_LEN=0 (pipeline for every size) and =4096
 (latency path up to 4 KiB); one JSON line per (values, value_bytes), host wall clock, median of 50 calls,
-every result checked against the first call's members and the values.
+every result checked against the first call's members and the values (a stability check for the timing,
+not parity: the reference's bytes for these calls are asserted by
+tests/test_gpu_codec.py::test_latency_path_batches_vs_reference and test_device_small_batches_vs_reference).
 
 usage: PMC_LATENCY_MAX_LEN=0 python scripts/few_sweep.py > few_0.jsonl
 """
