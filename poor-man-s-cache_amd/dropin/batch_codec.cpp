@@ -71,51 +71,42 @@ std::vector<StoredValue> CompressForSet(const std::vector<const char *> &values,
     return out;
 }
 
-std::vector<char *> DecompressForGet(const std::vector<Entry> &entries, std::vector<bool> *owned, pmc_ctx *ctx) {
-    const size_t n = entries.size();
-    std::vector<char *> out(n, nullptr);
-    if (owned) owned->assign(n, false);
-    std::vector<uint32_t> pick;
-    std::vector<uint64_t> src_off, dst_off;
-    std::vector<uint32_t> src_len, dst_cap;
-    uint64_t so = 0, dof = 0;
-    for (size_t i = 0; i < n; i++) {
-        const Entry &e = entries[i];
-        if (!e.compressed) {
-            out[i] = const_cast<char *>(e.data);
-            continue;
-        }
-        if (!e.data || e.size == 0) continue;  // Decompress's INVALID_INPUT -> nullptr
-        // ISIZE sizes the output (as GzipCompressor::Decompress); DEFLATE expands at most 1032:1
-        uint64_t cap = pmc_gzip_isize(e.data, e.size);
-        if (cap > 1032ull * e.size + 64) cap = 1032ull * e.size + 64;
-        pick.push_back((uint32_t)i);
-        src_off.push_back(so);
-        src_len.push_back((uint32_t)e.size);
-        dst_off.push_back(dof);
-        dst_cap.push_back((uint32_t)cap);
-        so += e.size;
+namespace {
+// The members k < n at src + src_off[k] (src_len[k] bytes each) decoded in one host call: out[k] a new[]
+// NUL-terminated value of olen[k] bytes, or nullptr (the reference's Decompress failure).  Capacity from
+// ISIZE (as GzipCompressor::Decompress), capped at DEFLATE's 1032:1.
+void decompress_packed(const uint8_t *src, const std::vector<uint64_t> &src_off, const std::vector<uint32_t> &src_len,
+                       std::vector<char *> &out, std::vector<uint32_t> &olen, pmc_ctx *ctx) {
+    const size_t n = src_len.size();
+    out.assign(n, nullptr);
+    olen.assign(n, 0);
+    if (!n) return;
+    std::vector<uint64_t> dst_off(n);
+    std::vector<uint32_t> dst_cap(n);
+    uint64_t dof = 0;
+    for (size_t k = 0; k < n; k++) {
+        uint64_t cap = pmc_gzip_isize(src + src_off[k], src_len[k]);
+        if (cap > 1032ull * src_len[k] + 64) cap = 1032ull * src_len[k] + 64;
+        dst_off[k] = dof;
+        dst_cap[k] = (uint32_t)cap;
         dof += cap;
     }
-    if (pick.empty()) return out;
-    std::vector<uint8_t> src(so), dst(dof + 1);
-    for (size_t k = 0; k < pick.size(); k++) memcpy(src.data() + src_off[k], entries[pick[k]].data, src_len[k]);
-    std::vector<uint32_t> dst_len(pick.size());
-    std::vector<int32_t> rc(pick.size(), 0);
+    std::vector<uint8_t> dst(dof + 1);
+    std::vector<uint32_t> dst_len(n);
+    std::vector<int32_t> rc(n, 0);
     if (!ctx) ctx = pmc_default_ctx();
-    int r = ctx ? pmc_gzip_decompress_batch_host(ctx, src.data(), src_off.data(), src_len.data(),
-                                                 (uint32_t)pick.size(), dst.data(), dst_off.data(), dst_cap.data(),
-                                                 dst_len.data(), rc.data())
-                : PMC_E_NO_DEVICE;
+    const int r = ctx ? pmc_gzip_decompress_batch_host(ctx, src, src_off.data(), src_len.data(), (uint32_t)n, dst.data(),
+                                                       dst_off.data(), dst_cap.data(), dst_len.data(), rc.data())
+                      : PMC_E_NO_DEVICE;
     auto place = [&](size_t k, const uint8_t *bytes, uint32_t len) {
         char *v = new char[len + 1];
         memcpy(v, bytes, len);
         v[len] = '\0';
-        out[pick[k]] = v;
-        if (owned) (*owned)[pick[k]] = true;
+        out[k] = v;
+        olen[k] = len;
     };
     std::vector<uint32_t> again;
-    for (size_t k = 0; k < pick.size(); k++) {
+    for (size_t k = 0; k < n; k++) {
         if (r) break;
         if (rc[k] == OPERATION_SUCCESS) place(k, dst.data() + dst_off[k], dst_len[k]);
         else if (rc[k] == PMC_E_CAPACITY && dst_len[k] > dst_cap[k]) again.push_back((uint32_t)k);
@@ -136,11 +127,43 @@ std::vector<char *> DecompressForGet(const std::vector<Entry> &entries, std::vec
             d2 += dst_len[k];
         }
         std::vector<uint8_t> dst2(d2 + 1);
-        const int r2 = pmc_gzip_decompress_batch_host(ctx, src.data(), s2_off.data(), s2_len.data(),
-                                                      (uint32_t)again.size(), dst2.data(), d2_off.data(),
-                                                      d2_cap.data(), d2_len.data(), rc2.data());
+        const int r2 = pmc_gzip_decompress_batch_host(ctx, src, s2_off.data(), s2_len.data(), (uint32_t)again.size(),
+                                                      dst2.data(), d2_off.data(), d2_cap.data(), d2_len.data(), rc2.data());
         for (size_t j = 0; j < again.size() && !r2; j++)
             if (rc2[j] == OPERATION_SUCCESS) place(again[j], dst2.data() + d2_off[j], d2_len[j]);
+    }
+}
+}  // namespace
+
+std::vector<char *> DecompressForGet(const std::vector<Entry> &entries, std::vector<bool> *owned, pmc_ctx *ctx) {
+    const size_t n = entries.size();
+    std::vector<char *> out(n, nullptr);
+    if (owned) owned->assign(n, false);
+    std::vector<uint32_t> pick;
+    std::vector<uint64_t> src_off;
+    std::vector<uint32_t> src_len;
+    uint64_t so = 0;
+    for (size_t i = 0; i < n; i++) {
+        const Entry &e = entries[i];
+        if (!e.compressed) {
+            out[i] = const_cast<char *>(e.data);
+            continue;
+        }
+        if (!e.data || e.size == 0) continue;  // Decompress's INVALID_INPUT -> nullptr
+        pick.push_back((uint32_t)i);
+        src_off.push_back(so);
+        src_len.push_back((uint32_t)e.size);
+        so += e.size;
+    }
+    if (pick.empty()) return out;
+    std::vector<uint8_t> src(so);
+    for (size_t k = 0; k < pick.size(); k++) memcpy(src.data() + src_off[k], entries[pick[k]].data, src_len[k]);
+    std::vector<char *> vals;
+    std::vector<uint32_t> olen;
+    decompress_packed(src.data(), src_off, src_len, vals, olen, ctx);
+    for (size_t k = 0; k < pick.size(); k++) {
+        out[pick[k]] = vals[k];
+        if (owned && vals[k]) (*owned)[pick[k]] = true;
     }
     return out;
 }
@@ -311,7 +334,6 @@ void BeginCollect() {
 void PrimeCollected(pmc_ctx *ctx) {
     PrimeState &P = g_prime;
     P.collecting = false;
-    std::vector<Entry> ents;
     std::vector<uint32_t> which;
     for (const auto &c : P.collected) {
         auto seen = P.didx.find(c.first);
@@ -327,9 +349,17 @@ void PrimeCollected(pmc_ctx *ctx) {
     }
     P.collected.clear();
     if (which.empty()) return;
-    for (uint32_t idx : which) ents.push_back({P.dmembers.data() + P.dec[idx].off, P.dec[idx].size, true});
-    std::vector<bool> owned;
-    std::vector<char *> vals = DecompressForGet(ents, &owned, ctx);
+    // (straight from dmembers, where the members already lie back to back; the decoded lengths come back
+    // with the values, no strlen over them)
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> len;
+    for (uint32_t idx : which) {
+        off.push_back(P.dec[idx].off);
+        len.push_back((uint32_t)P.dec[idx].size);
+    }
+    std::vector<char *> vals;
+    std::vector<uint32_t> olen;
+    decompress_packed((const uint8_t *)P.dmembers.data(), off, len, vals, olen, ctx);
     P.stats.batches++;
     for (size_t k = 0; k < which.size(); k++) {
         auto &d = P.dec[which[k]];
@@ -338,7 +368,7 @@ void PrimeCollected(pmc_ctx *ctx) {
             continue;
         }
         d.data = vals[k];
-        d.len = strlen(vals[k]);
+        d.len = olen[k];  // (a value with an embedded NUL: its copies still read as the same C string)
     }
 }
 
