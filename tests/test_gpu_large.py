@@ -107,3 +107,16 @@ def test_block_edges(ctx, D, large_golden):
     """A parse ending exactly on a 16383-symbol boundary with a literal (zlib: no flush for the last literal, the
     final block holds 16383 symbols), and random bytes around one and two blocks (stored blocks)."""
     _check(ctx, D, LV.block_edges(), large_golden)
+
+
+def test_mid_size_small_batches_take_the_large_pass(ctx, D, golden, large_golden):
+    """Values of 16,383-32,506 B: a batch of at most 2 values per CU whose values all fit the split pipeline's
+    large pass keeps it (a lone 30 KB value: 5 ms there, 10 ms through the large-value pipeline); bigger
+    batches take the large-value pipeline (the 100K x 30 KB bench leg, digest-checked).  Every reference
+    vector of that size class, in batches of 1, 7 and all of them, against the reference's members.  Values
+    of several DEFLATE blocks (random bytes) are redone by the HBM kernel here, so no retry-counter check."""
+    vals = [v for sets in LV.all_sets(golden.corpus).values() for v in sets if 16383 <= len(v) <= 32506]
+    assert len(vals) >= 15, len(vals)
+    for m in (1, 7, len(vals)):
+        for k in range(0, len(vals), m):
+            _check(ctx, D, vals[k:k + m], large_golden, may_fall_back=True)
