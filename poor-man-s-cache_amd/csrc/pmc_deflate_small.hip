@@ -119,29 +119,12 @@ struct FrontLayout {
     int pkb;             // chain-count bits packed into R's top (front_pkb), 0: CN array, -1: HC only
     uint64_t cn, hc, ev; // parse scratch in X (cn unused when pk); the sort's 512-B table at X
 };
-// PMC_FRONT_S10: at values of <= 1 KiB (pkb 6) the sorted positions (< 1024, 10 bits) are packed three
-// to a word, which takes the front's LDS from 5,696 to 5,008 B per wave: 32 resident waves per CU (8 per
-// SIMD) instead of 28, with the kernel held to 64 VGPRs (pmc_deflate_split.hip).  The region keeps at
-// least 256 B: the sort parks its 128 high-digit counters there (sort_positions2_body).
-#ifndef PMC_FRONT_S10
-#define PMC_FRONT_S10 0
-#endif
-__host__ __device__ inline bool front_s10(uint64_t n) { return PMC_FRONT_S10 && front_pkb(n) == 6; }
-// PMC_SPLIT_MT: at values of <= 1 KiB the split front writes only its matches to the token slab, one
-// 28-bit record each (position << 18 | distance - 1 << 8 | length - 3), and the literals stay implicit
-// (every position no match covers); the front's histogram and the back's emission rebuild them from a
-// coverage bitmap.  The slab shrinks from one word per token to one per match.
-#ifndef PMC_SPLIT_MT
-#define PMC_SPLIT_MT 0
-#endif
-__host__ __device__ inline bool split_mt(uint64_t n) { return PMC_SPLIT_MT && n <= 1024; }
 __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
     auto a = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
     FrontLayout F;
     F.bytes = 0;
     F.S = a(n + 32);
-    const uint64_t s_bytes = front_s10(n) ? (((n + 2) / 3) * 4 > 256 ? ((n + 2) / 3) * 4 : 256) : 2 * n + 2;
-    F.R = F.S + a(s_bytes);
+    F.R = F.S + a(2 * n + 2);
     F.X = F.R + a(2 * n + 2);
     F.pkb = front_pkb(n);
     F.cn = F.X;
@@ -305,50 +288,7 @@ struct TreeOut {
 
 // chain candidates evaluated per position by the on-demand parse's wave step (the rest, when
 // needed, by search()); at most 32 (5-bit field in the eval key)
-#ifndef PMC_PRECAND
-#define PMC_PRECAND 32
-#endif
-// PMC_FRONT_GAP (k > 0): an eval window first compares every position with its nearest chain candidate
-// (16 bytes), follows the lazy parse's likely path through the first k predicted matches and gives no
-// lanes to the positions inside them; the nearest candidate's result seeds each position's maximum, so
-// a position with one candidate needs no lane at all.  0: lanes for every has-candidate position.
-#ifndef PMC_FRONT_GAP
-#define PMC_FRONT_GAP 0
-#endif
-// PMC_EVAL_SEGMAX: at <= 4 KiB the eval's per-position maximum by a segmented max-scan, not LDS atomics
-#ifndef PMC_EVAL_SEGMAX
-#define PMC_EVAL_SEGMAX 1
-#endif
-// PMC_FRONT_INLINE: the sort and the parse inlined into their kernels, so the wave state never lives in
-// scratch (noinline calls took `this` and copied the state from there: round 4 measured the front's
-// writes at 3.3 KB per 1 KiB value that way, 2.3 KB inlined, at the same speed)
-#ifndef PMC_FRONT_INLINE
-#define PMC_FRONT_INLINE 1
-#endif
-#if PMC_FRONT_INLINE
-#define PMC_NOINLINE_FRONT __forceinline__
-#else
-#define PMC_NOINLINE_FRONT __noinline__
-#endif
-// PMC_HC_BALLOT: build_cn writes the has-candidate bits by a ballot pass over the counts, not lds_or
-#ifndef PMC_HC_BALLOT
-#define PMC_HC_BALLOT 0
-#endif
-// PMC_SORT_AGG: (with PMC_SORT_U32) the chunk's lanes sharing lane 0's digit take one atomic together
-#ifndef PMC_SORT_AGG
-#define PMC_SORT_AGG 0
-#endif
-// PMC_SORT_U32: the hash sort's digit counters one u32 per digit (sort_positions2_body)
-#ifndef PMC_SORT_U32
-#define PMC_SORT_U32 1
-#endif
-// PMC_LDS_B64: the 16-byte window loads (load16) as three aligned ds_read_b64
-#ifndef PMC_SORT_REG
-#define PMC_SORT_REG 0 // register-resident bitonic sort + ranks for 512 < npos <= 1024 (SmallWave::sort_rank_reg; measured slower)
-#endif
-#ifndef PMC_LDS_B64
-#define PMC_LDS_B64 0
-#endif
+constexpr uint32_t kPreCandLanes = 32;
 // A uniform 0/1 integer the compiler may not turn back into a bool: branching on it is one
 // s_cmp + s_cbranch_scc.  (Bools merged across blocks become 64-bit lane masks -- s_cselect_b64,
 // s_and_b64 with exec, s_cbranch_vcc -- on the scalar unit, which the parse saturates.)
@@ -358,154 +298,11 @@ __device__ __forceinline__ uint32_t sflag(uint32_t x) {
     return x;
 }
 
-// ---- register-resident sort of a value's positions by hash (SmallWave::sort_rank_reg) -----------------
-// (a function of its own: inlined into the front, its 16 key registers raised the parse loop's spills)
-template <int M>
-__device__ __forceinline__ uint32_t xlane(uint32_t v) { // the value of lane l ^ M, M <= 8
-    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
-    else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
-    else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
-    else {
-        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false); // lane l - 4
-        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12C, 0xF, 0xF, false); // lane l + 4
-        return (lane_id() & 4) ? dn : up;
-    }
-}
-template <int P, int K, int J>
-struct Bitonic {
-    // one stage (K, J) of the network, then the rest
-    __device__ static __forceinline__ void run(uint32_t (&x)[P], uint32_t l) {
-        if constexpr (J < P) {
-#pragma unroll
-            for (int r = 0; r < P; r++) {
-                if (r & J) continue;
-                const bool asc = (((uint32_t)P * l + (uint32_t)r) & (uint32_t)K) == 0;
-                const uint32_t a = x[r], b = x[r | J];
-                const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-                x[r] = asc ? lo : hi;
-                x[r | J] = asc ? hi : lo;
-            }
-        } else if constexpr (J / P <= 8) {
-            constexpr int M = J / P;
-            // (K > J >= P: the direction is lane-uniform, (P l) & K; the lower lane keeps the min iff ascending)
-            const bool take_min = ((l & (uint32_t)M) == 0) == ((((uint32_t)P * l) & (uint32_t)K) == 0);
-#pragma unroll
-            for (int r = 0; r < P; r++) {
-                const uint32_t y = xlane<M>(x[r]);
-                const uint32_t lo = x[r] < y ? x[r] : y, hi = x[r] < y ? y : x[r];
-                x[r] = take_min ? lo : hi;
-            }
-        } else {
-            constexpr int M = J / P; // 16 or 32: registers 2t, 2t + 1 swap halves, each lane takes one pair
-            const uint32_t low = l & ~(uint32_t)M;
-            const bool asc = (((uint32_t)P * low) & (uint32_t)K) == 0;
-#pragma unroll
-            for (int t = 0; t < P; t += 2) {
-                auto s = M == 16 ? __builtin_amdgcn_permlane16_swap(x[t], x[t + 1], false, false)
-                                 : __builtin_amdgcn_permlane32_swap(x[t], x[t + 1], false, false);
-                const uint32_t a = s[0], b = s[1];
-                const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
-                auto u = M == 16 ? __builtin_amdgcn_permlane16_swap(asc ? lo : hi, asc ? hi : lo, false, false)
-                                 : __builtin_amdgcn_permlane32_swap(asc ? lo : hi, asc ? hi : lo, false, false);
-                x[t] = u[0];
-                x[t + 1] = u[1];
-            }
-        }
-        if constexpr (J > 1) Bitonic<P, K, J / 2>::run(x, l);
-        else if constexpr (K < 64 * P) Bitonic<P, K * 2, K>::run(x, l);
-    }
-};
-template <int P, int PK>
-__device__ __noinline__ uint32_t sort_rank_reg_fn(PMC_LDS const uint32_t *bw, PMC_LDS uint16_t *S, PMC_LDS uint16_t *R,
-                                                  PMC_LDS uint64_t *HC, uint32_t npos_) {
-    static_assert(P == 16 && PK == 6, "ranks of 10 bits, counts in R's top 6 bits");
-    constexpr uint32_t RB = 16 - PK, CMAX = (1u << PK) - 1;
-    const uint32_t npos = rfl(npos_);
-    const uint32_t l = (uint32_t)lane_id(), e0 = (uint32_t)P * l;
-    // keys: bytes P l .. P l + P + 2 are dwords P / 4 l .. P / 4 l + P / 4 (one 16-byte and one 4-byte read)
-    uint32_t w[P / 4 + 1];
-    {
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        const v4u q = *(PMC_LDS const v4u *)(bw + (P / 4) * l);
-        w[0] = q.x;
-        w[1] = q.y;
-        w[2] = q.z;
-        w[3] = q.w;
-        w[4] = bw[(P / 4) * l + 4];
-    }
-    uint32_t x[P];
-#pragma unroll
-    for (int r = 0; r < P; r++) {
-        const uint32_t b4 = __builtin_amdgcn_alignbyte(w[(r >> 2) + 1], w[r >> 2], (uint32_t)(r & 3));
-        x[r] = e0 + (uint32_t)r < npos ? hash3(b4) << 10 | (e0 + (uint32_t)r) : 0xffffffffu;
-    }
-    // HC words to zero while the network runs (ordered before the lds_or below by the wave_sync)
-    for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
-    Bitonic<P, 2, 1>::run(x, l);
-    // sorted: element e0 + r in x[r].  Position 0's rank; run starts (a new hash) and the chain count
-    // of each entry: the entries before it in its run, less position 0 (zlib's NIL, first of its run)
-    uint32_t kz = 0;
-#pragma unroll
-    for (int r = 0; r < P; r++) kz = (x[r] & 1023u) == 0u && x[r] != 0xffffffffu ? e0 + (uint32_t)r + 1u : kz;
-    const uint32_t k0 = wave_max_dpp(kz) - 1u;
-    uint32_t prev0 = (uint32_t)__shfl_up((int)(x[P - 1] >> 10), 1);
-    prev0 = l == 0 ? 0xffffffffu : prev0;
-    uint32_t last = 0;
-    {
-        uint32_t prev = prev0;
-#pragma unroll
-        for (int r = 0; r < P; r++) {
-            const uint32_t h = x[r] >> 10;
-            last = e0 + (uint32_t)r < npos && h != prev ? e0 + (uint32_t)r : last;
-            prev = h;
-        }
-    }
-    // the run start in force at the lane's first entry: the last start of the lanes below
-    uint32_t carry = (uint32_t)__shfl_up((int)wave_incl_max_dpp(last), 1);
-    carry = l == 0 ? 0u : carry;
-    wave_sync();
-    // S in sorted order (two 16-byte stores per lane while the lane's entries are all real)
-    if (e0 + P <= npos) {
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        uint32_t pk[P / 2];
-#pragma unroll
-        for (int r = 0; r < P / 2; r++) pk[r] = (x[2 * r] & 1023u) | (x[2 * r + 1] & 1023u) << 16;
-        *(PMC_LDS v4u *)(S + e0) = v4u{pk[0], pk[1], pk[2], pk[3]};
-        *(PMC_LDS v4u *)(S + e0 + 8) = v4u{pk[4], pk[5], pk[6], pk[7]};
-    } else {
-#pragma unroll
-        for (int r = 0; r < P; r++)
-            if (e0 + (uint32_t)r < npos) S[e0 + r] = (uint16_t)(x[r] & 1023u);
-    }
-    uint32_t rs = carry, prev = prev0;
-#pragma unroll
-    for (int r = 0; r < P; r++) {
-        const uint32_t e = e0 + (uint32_t)r, h = x[r] >> 10;
-        rs = e < npos && h != prev ? e : rs;
-        prev = h;
-        if (e < npos) {
-            const uint32_t p = x[r] & 1023u;
-            const uint32_t cnt = e - rs - (rs == k0 && e > rs ? 1u : 0u);
-            R[p] = (uint16_t)(e | (cnt < CMAX ? cnt : CMAX) << RB);
-            if (cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
-        }
-    }
-    wave_sync();
-    return k0 | 0x80000000u; // (SmallWave::kRanked)
-}
-
-
 struct SmallWave {
     // every working array is LDS-typed (ds_* with 32-bit addresses)
     PMC_LDS uint8_t *b;
     PMC_LDS uint32_t *bw;
     PMC_LDS uint16_t *S, *R;
-#if PMC_FRONT_S10
-    uint32_t s10 = 0; // front at <= 1 KiB (front_s10): S packed three 10-bit positions per word (sget)
-#endif
-#if PMC_SPLIT_MT
-    uint32_t mt = 0;  // split front/back at <= 1 KiB (split_mt): the slab holds match records only
-#endif
     PMC_LDS uint32_t *lfreq, *dfreq, *blfreq;
     PMC_LDS uint32_t *outw;
     PMC_LDS uint8_t *outb;
@@ -553,15 +350,10 @@ struct SmallWave {
 #define PMC_STOP(k, ret)
 #endif
 
-    // sorted position k: packed (PK 6 with PMC_FRONT_S10: entry k is bits 10 (k % 3) .. of word k / 3) or u16
+    // sorted position k
     template <int PK>
     __device__ __forceinline__ uint32_t sget(uint32_t k) const {
-        if constexpr (PK == 6 && PMC_FRONT_S10) {
-            const uint32_t w = __umul24(k, 0xAAABu) >> 17; // k / 3 for k < 98304
-            return (((PMC_LDS const uint32_t *)S)[w] >> (10 * (k - 3 * w))) & 1023u;
-        } else {
-            return S[k];
-        }
+        return S[k];
     }
     __device__ uint32_t load4(uint32_t p) const {
         uint32_t w0 = bw[p >> 2], w1 = bw[(p >> 2) + 1];
@@ -627,7 +419,7 @@ struct SmallWave {
     // the scatter is stable without per-lane counters or a ballot per digit bit.
     // Returns the rank of position 0 (the number of positions whose hash is smaller: the sort is
     // stable and 0 is the lowest position); the rank array R itself is written by build_cn.
-    __device__ PMC_NOINLINE_FRONT uint32_t sort_positions2(uint32_t npos_, PMC_LDS uint32_t *tab) {
+    __device__ __forceinline__ uint32_t sort_positions2(uint32_t npos_, PMC_LDS uint32_t *tab) {
         SmallWave me = *this; // (see parse_ondemand)
         return me.sort_positions2_body(npos_, tab);
     }
@@ -644,33 +436,17 @@ struct SmallWave {
         // shorter values count per pass.)
         PMC_LDS uint32_t *hiw = (PMC_LDS uint32_t *)S;
         const bool fused = npos >= 128;
-#if PMC_SORT_U32
-        // PMC_SORT_U32: one u32 counter per digit instead of two u16 per word (digits d and d ^ 1 no longer
-        // share an address, so fewer lanes of a returning atomic serialise on one word): the 256 low-digit
+        // One u32 counter per digit instead of two u16 per word (digits d and d ^ 1 no longer share an
+        // address, so fewer lanes of a returning atomic serialise on one word): the 256 low-digit
         // counters in S (free until the second scatter), the 128 high-digit ones in tab
         // (values of 512 .. 1024 bytes: S then spans at least 1 KiB, the cap's 2 * cap + 2 bytes)
-        if (!PMC_FRONT_S10 && npos >= 510 && npos <= 1022) {
+        if (npos >= 510 && npos <= 1022) {
             PMC_LDS uint32_t *cl = (PMC_LDS uint32_t *)S;
             for (uint32_t k = l; k < 256; k += 64) cl[k] = 0;
             for (uint32_t k = l; k < 128; k += 64) tab[k] = 0;
             wave_sync();
-            // (PMC_SORT_AGG: lane 0's digit is taken once for all the chunk's lanes that share it -- runs of
-            // one byte, JSON indentation, put many lanes of an instruction on one counter, and the LDS
-            // serialises same-address atomics)
-            const uint64_t below = (1ull << l) - 1ull;
             auto agg_add = [&](PMC_LDS uint32_t *ctr, uint32_t d, bool valid) -> uint32_t {
-#if PMC_SORT_AGG
-                const uint32_t d0 = readlane(d, 0);
-                const uint64_t m = ballot(valid && d == d0);
-                const bool inm = (m >> l) & 1ull;
-                const uint32_t lead = m ? (uint32_t)__builtin_ctzll(m) : 0u;
-                uint32_t old = 0;
-                if (valid && (!inm || l == lead)) old = lds_add(&ctr[d], inm ? (uint32_t)__builtin_popcountll(m) : 1u);
-                const uint32_t base = readlane(old, (int)lead);
-                return inm ? base + (uint32_t)__builtin_popcountll(m & below) : old;
-#else
                 return valid ? lds_add(&ctr[d], 1u) : 0u;
-#endif
             };
             for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
                 const uint32_t x = c0 + l;
@@ -714,7 +490,6 @@ struct SmallWave {
             }
             return k0;
         }
-#endif
         auto scan_tab = [&]() { // 256 counters -> exclusive bases
             const uint32_t t0 = tab[2 * l], t1 = tab[2 * l + 1];
             const uint32_t v0 = t0 & 0xffffu, v1 = t0 >> 16, v2 = t1 & 0xffffu, v3 = t1 >> 16;
@@ -743,11 +518,6 @@ struct SmallWave {
             hiw[l] = c0 | (c0 + u0) << 16;
             wave_sync();
         }
-#if PMC_FRONT_S10
-        const uint32_t pk10 = s10; // (packed S: the second scatter ORs 10-bit fields into zeroed words)
-#else
-        constexpr uint32_t pk10 = 0;
-#endif
         for (int pass = 0; pass < 2; pass++) {
             const uint32_t sh = pass ? 8 : 0;
             PMC_LDS uint16_t *dst = pass ? S : Tt;
@@ -769,10 +539,6 @@ struct SmallWave {
                 scan_tab();
                 wave_sync();
             }
-            if ((uint32_t)pass & pk10) {
-                for (uint32_t k = l; k < (npos + 2) / 3; k += 64) ((PMC_LDS uint32_t *)S)[k] = 0u;
-                wave_sync();
-            }
             // a lane's slot from one returning LDS atomic on its digit's counter: the lanes of one
             // ds_add_rtn to a word get their old values in lane order (scripts/micro/
             // lds_atomic_order.hip: 16.7M trials of skewed digit mixes, none out of order), so the
@@ -787,36 +553,12 @@ struct SmallWave {
                 const uint32_t d = (hash3(load4(p)) >> sh) & 255, hs = 16 * (d & 1);
                 if (x < npos) {
                     const uint32_t slot = (lds_add(&tab[d >> 1], 1u << hs) >> hs) & 0xffffu;
-                    if ((uint32_t)pass & pk10) {
-                        const uint32_t w = __umul24(slot, 0xAAABu) >> 17;
-                        lds_or((PMC_LDS uint32_t *)S + w, p << (10 * (slot - 3 * w)));
-                    } else {
-                        dst[slot] = (uint16_t)p;
-                    }
+                    dst[slot] = (uint16_t)p;
                 }
             }
             wave_sync();
         }
         return k0;
-    }
-
-    // ---- register-resident sort of the positions by hash, with their ranks and chain counts -----------
-    // For 512 < npos <= 64 P: lane l holds the keys hash << 10 | position of positions P l .. P l + P - 1
-    // (~0 past npos) in P registers and a bitonic network sorts the wave's 64 P keys, element e = P l + r
-    // in register r of lane l.  Compare-exchanges between registers of one lane are plain min / max;
-    // between lanes l and l ^ m: m = 1, 2 quad_perm DPP, m = 8 row_ror:8, m = 4 row_ror:4 / row_ror:12
-    // (lane l reads lane l - n of its row under row_ror:n), m = 16, 32 v_permlane16/32_swap, which
-    // bring both keys of a pair into one lane for two registers at once and back.  The key order is
-    // (hash, position): the stable order the radix sort produced, by construction, with no LDS
-    // atomics -- the returning atomics of sort_positions2 serialised on repeated trigrams (~1,900
-    // bank-conflict cycles per 1 KiB value, profiles/r04/front) and needed the lane-order guard.  From
-    // the sorted registers the same pass writes S (2 x 16-byte stores per lane), the ranks with their
-    // packed chain counts R and the has-candidate bits HC, which build_cn made from a second walk over
-    // S.  Returns k0 (position 0's rank) | kRanked.
-    static constexpr uint32_t kRanked = 0x80000000u;
-    template <int P, int PK>
-    __device__ __forceinline__ uint32_t sort_rank_reg(uint32_t npos) {
-        return sort_rank_reg_fn<P, PK>(bw, S, R, HC, npos);
     }
 
     // 8 bytes at p (dword-aligned LDS reads + alignbyte; the value is zero padded)
@@ -860,7 +602,7 @@ struct SmallWave {
     // parallel before the serial parse.  M[i] = best | bestq << 9 | (walk cut short) << 31
     // with best = max over those candidates of min(LCP, nice), bestq the nearest achieving
     // it.  A cut-short walk is finished by search() if the parse visits i.
-    static constexpr uint32_t kPreCand = PMC_PRECAND;
+    static constexpr uint32_t kPreCand = kPreCandLanes;
     // Work-stealing walk, branch-light: every iteration each lane issues the same loads
     // (one chain entry, 8 bytes at i+off and at c+off, the two prune words) and advances
     // its state with selects -- a candidate is fetched, pruned, or compared 8 bytes further.
@@ -1119,11 +861,8 @@ struct SmallWave {
         const uint32_t l = (uint32_t)lane_id();
         // has-candidate bits set by position below (HC as u32 words, LDS atomics): no second
         // pass over the positions
-        constexpr bool kHcPass = PMC_HC_BALLOT && PK >= 0; // (HC from the counts afterwards, by ballot)
-        if (!kHcPass) {
-            for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
-            wave_sync();
-        }
+        for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
+        wave_sync();
         uint32_t ph = 0xffffffffu, prs = 0, pq = 0; // previous chunk's last hash, run start, position
         uint32_t bad = 0;
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
@@ -1142,24 +881,13 @@ struct SmallWave {
             if (valid) { // (the rank array R is written here, not by the sort)
                 R[p] = (uint16_t)(PK > 0 ? k | (cnt < CMAX ? cnt : CMAX) << RB : k);
                 if (PK == 0) CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
-                if (!kHcPass && cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
+                if (cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
             }
             ph = readlane(h, 63);
             prs = readlane(rs, 63);
             pq = readlane(p, 63);
         }
         wave_sync();
-        if constexpr (kHcPass) {
-            // has-candidate bits in position order: a ballot of the counts per 64 positions, stored by one
-            // lane (no same-word atomics from lanes of one hash run)
-            for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
-                const uint32_t x = c0 + l;
-                const uint32_t c = x < npos ? (PK > 0 ? (uint32_t)R[x] >> RB : (uint32_t)CN[x]) : 0u;
-                const uint64_t m = ballot(c != 0u);
-                if (l == 0) HC[c0 >> 6] = m;
-            }
-            wave_sync();
-        }
         return ballot(bad != 0u) ? 1u : 0u;
     }
     // results of the current eval: window start p0, evaluated offsets m (uniform) and, in
@@ -1185,22 +913,7 @@ struct SmallWave {
     // 16 bytes at p as two 8-byte words (5 dword reads + alignbyte)
     __device__ void load16(uint32_t p, uint64_t &lo, uint64_t &hi) const {
         const uint32_t w = p >> 2, sh = p & 3;
-#if PMC_LDS_B64
-        // three 8-byte aligned ds_read_b64 (64 banks, 2 LDS cycles each) instead of five ds_read_b32 (32 banks):
-        // dwords e .. e + 5 of the even e <= w, the five needed picked by w's parity
-        const uint32_t e = w >> 1, od = w & 1u;
-        PMC_LDS const uint64_t *b8 = (PMC_LDS const uint64_t *)bw;
-        // (indices the compiler cannot relate: adjacent ones it merges into ds_read2_b64, 8 LDS cycles for
-        // the two instead of 4)
-        uint32_t e1 = e + 1, e2 = e + 2;
-        asm volatile("" : "+v"(e1), "+v"(e2));
-        const uint64_t x0 = b8[e], x1 = b8[e1], x2 = b8[e2];
-        const uint32_t d0 = (uint32_t)x0, d1 = (uint32_t)(x0 >> 32), d2 = (uint32_t)x1, d3 = (uint32_t)(x1 >> 32);
-        const uint32_t d4 = (uint32_t)x2, d5 = (uint32_t)(x2 >> 32);
-        const uint32_t w0 = od ? d1 : d0, w1 = od ? d2 : d1, w2 = od ? d3 : d2, w3 = od ? d4 : d3, w4 = od ? d5 : d4;
-#else
         const uint32_t w0 = bw[w], w1 = bw[w + 1], w2 = bw[w + 2], w3 = bw[w + 3], w4 = bw[w + 4];
-#endif
         lo = (uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32 | __builtin_amdgcn_alignbyte(w1, w0, sh);
         hi = (uint64_t)__builtin_amdgcn_alignbyte(w4, w3, sh) << 32 | __builtin_amdgcn_alignbyte(w3, w2, sh);
     }
@@ -1236,68 +949,27 @@ struct SmallWave {
         cn = x < npos ? cn : 0u;
         cn1 = x + 1 < npos ? cn1 : 0u;
         const uint32_t w0 = SAT && cn == CMAX ? kPreCand : cn < kPreCand ? cn : kPreCand;
-#if PMC_FRONT_GAP
-        // (a) nearest candidate of every offset: q1 = S[R - 1] (a count >= 1 excludes NIL, so the entry
-        // before a position in the hash order is its nearest candidate), 16 bytes compared
-        uint32_t q1 = sget<PK>(cn != 0u ? rx - 1u : 0u);
-        uint64_t X0, X1, Q0, Q1;
-        load16(xc, X0, X1);
-        load16(q1, Q0, Q1);
-        const uint32_t nx1 = (len - xc) < 258 ? (len - xc) : 258;
-        uint32_t f1 = eq_bytes8(X0 ^ Q0);
-        f1 = f1 + (f1 >> 3) * eq_bytes8(X1 ^ Q1);
-        const uint32_t fx = cn != 0u && (f1 < 16u || nx1 <= 16u) ? 1u : 0u; // f1 is q1's exact length
-        f1 = f1 < nx1 ? f1 : nx1;
-        // (b) the lazy parse's likely path from offset 0: at a predicted match j (f1 >= 3, TOO_FAR
-        // respected; j + 1 when that one is longer) the positions j + 2 .. j + f1 - 1 get no lanes
-        const uint64_t jm = ballot(cn != 0u && f1 >= 3u && (f1 > 3u || xc - q1 <= 4096u));
-        uint64_t skip = 0;
-        uint32_t o = 0;
-        for (int it = 0; it < PMC_FRONT_GAP && o < 64; it++) {
-            const uint64_t mj = jm & (~0ull << o);
-            if (!mj) break;
-            uint32_t j = (uint32_t)__builtin_ctzll(mj), fj = readlane(f1, (int)j);
-            if (j < 63 && ((jm >> (j + 1)) & 1)) {
-                const uint32_t fn = readlane(f1, (int)j + 1);
-                j += fn > fj ? 1u : 0u;
-                fj = fn > fj ? fn : fj;
-            }
-            o = j + fj;
-            if (j + 2 < 64) skip |= (o >= 64 ? ~0ull : (1ull << o) - 1) & (~0ull << (j + 2));
-        }
-        const uint32_t sk = (uint32_t)(skip >> l) & 1u;
-        // (c) lanes: the candidates after the nearest where its result is exact
-        const uint32_t w = sk ? 0u : w0 - fx;
-        const bool fre = fx != 0u && w0 == 1u; // one candidate, compared in (a): evaluated without lanes
-#else
-        const uint32_t w = w0, fx = 0;
-        const bool fre = false;
-#endif
+        const uint32_t w = w0;
         const uint32_t incl = wave_incl_scan_dpp(w), offs = incl - w;
         const bool inc = w != 0 && incl <= 64;
-        const uint64_t iml = ballot(inc); // lane-owning offsets
-        const uint64_t im = iml | ballot(fre); // evaluated offsets
-        const uint32_t nl = iml ? readlane(incl, 63 - __builtin_clzll(iml)) : 0u;
+        const uint64_t im = ballot(inc); // evaluated (lane-owning) offsets
+        const uint32_t nl = im ? readlane(incl, 63 - __builtin_clzll(im)) : 0u;
 #ifdef PMC_STAMPS
         st[7] += nl; // (stamps build: lanes used per eval)
 #endif
-        // first lane of each evaluated offset j: offs << 26 | (j + 1) << 19 | fx << 18 | R (offs
-        // grows with j, so a max-scan hands every lane its owner); other lanes store to dummy slots
+        // first lane of each evaluated offset j: offs << 26 | (j + 1) << 19 | R (offs grows with j,
+        // so a max-scan hands every lane its owner); other lanes store to dummy slots
         PMC_LDS uint32_t *dmy = EV + 64; // (the u8 mark area, 16 words)
         EV[l] = 0;
-        (inc ? EV : dmy)[inc ? offs : (l & 15)] = offs << 26 | (l + 1) << 19 | fx << 18 | rx;
+        (inc ? EV : dmy)[inc ? offs : (l & 15)] = offs << 26 | (l + 1) << 19 | rx;
         wave_sync();
         const uint32_t mk = EV[l];
         // (LDS keeps one wave's accesses in order: the read above sees the marks)
-#if PMC_FRONT_GAP
-        EV[l] = fx ? f1 << 23 | (kPreCand - 1u) << 18 | q1 : 0u; // the nearest candidate's key
-#else
         EV[l] = 0;
-#endif
         const bool v = l < nl;
         const uint32_t sc = wave_incl_max_dpp(mk);
         const uint32_t own = v ? ((sc >> 19) & 127) - 1 : 0u;
-        const uint32_t P = p0 + own, d = l - (sc >> 26) + 1 + ((sc >> 18) & 1u);
+        const uint32_t P = p0 + own, d = l - (sc >> 26) + 1;
         const uint32_t rxo = sc & 0xffffu;
         uint32_t q = sget<PK>(v && (!SAT || rxo >= d) ? rxo - d : 0u);
         uint64_t A0, A1, B0, B1;
@@ -1335,7 +1007,6 @@ struct SmallWave {
             off += 16;
         }
         cl = cl < nice ? cl : nice;
-#if PMC_EVAL_SEGMAX
         if (sflag(len <= 4096 ? 1u : 0u)) {
             // An offset's lanes are contiguous and own grows with the lane: an inclusive max-scan of
             // own << 26 | (cl, nearness, q) leaves each offset's maximum in its last lane, which stores it.
@@ -1348,9 +1019,7 @@ struct SmallWave {
                 const uint32_t m = mx & 0x3ffffffu;
                 EV[own] = (m >> 17) << 23 | ((m >> 12) & 31u) << 18 | (m & 4095u);
             }
-        } else
-#endif
-        {
+        } else {
             __hip_atomic_fetch_max(&EV[own], vk ? cl << 23 | (kPreCand - d) << 18 | q : 0u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WAVEFRONT);
         }
@@ -1426,13 +1095,6 @@ struct SmallWave {
     // stores its run and itself with lane-parallel stores (lane k: token n + k), and the tail run
     // [lf, len) goes out at the end -- no per-literal bookkeeping on the scalar unit.
     __device__ void tb_match(TokBuf &t, uint32_t lf, uint32_t s, uint32_t m) {
-#if PMC_SPLIT_MT
-        if (sflag(mt)) { // match record only (m = distance << 16 | length - 3)
-            if (lane_id() == 0) tok[t.n] = s << 18 | ((m >> 16) - 1u) << 8 | (m & 0xffu);
-            t.n++;
-            return;
-        }
-#endif
         const uint32_t l = (uint32_t)lane_id(), nl = s - lf, cnt = nl + 1;
         // first 64 tokens with every lane storing (no exec mask work on the scalar unit): lanes
         // past the run repeat the match token at its own slot, so no byte past it is written
@@ -1449,9 +1111,6 @@ struct SmallWave {
         t.n += cnt;
     }
     __device__ void tb_lits(TokBuf &t, uint32_t lf, uint32_t e) {
-#if PMC_SPLIT_MT
-        if (sflag(mt)) return; // (implicit literals)
-#endif
         const uint32_t l = (uint32_t)lane_id(), cnt = e - lf;
         for (uint32_t b = 0; b < cnt; b += 64) {
             const uint32_t k = b + l;
@@ -1474,7 +1133,7 @@ struct SmallWave {
     // member pointer would be re-read from memory inside the loop.  A local copy lives in SGPRs.)
     template <int PK>
     // (k0_: the rank of position 0, from sort_positions2; build_cn needs it before R exists)
-    __device__ PMC_NOINLINE_FRONT uint32_t parse_ondemand(uint32_t npos_, uint32_t len_, uint32_t k0_) {
+    __device__ __forceinline__ uint32_t parse_ondemand(uint32_t npos_, uint32_t len_, uint32_t k0_) {
         SmallWave me = *this;
         const uint32_t r = me.parse_ondemand_body<PK>(npos_, len_, k0_);
 #ifdef PMC_STAMPS
@@ -1487,8 +1146,7 @@ struct SmallWave {
     __device__ __forceinline__ uint32_t parse_ondemand_body(uint32_t npos_, uint32_t len_, uint32_t k0_) {
         const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
         const uint32_t nw = (npos + 63) >> 6;
-        if (!PMC_SORT_REG || !(rfl(k0_) & kRanked)) // (sort_rank_reg built R and HC itself)
-            if (sflag(build_cn<PK>(npos, rfl(k0_)))) return kNtokRetry; // (the sort's lane-order guard)
+        if (sflag(build_cn<PK>(npos, rfl(k0_)))) return kNtokRetry; // (the sort's lane-order guard)
         stamp(11);
         PMC_STOP(13, 0)
         Group g;
@@ -2202,12 +1860,6 @@ struct SmallWave {
     // ---- split pipeline pieces (pmc_deflate_split.hip) ----------------------------------------
     // histogram of the token slab into lfreq / dfreq (END_BLOCK counted once)
     __device__ void histogram(uint32_t ntok, uint32_t len) {
-#if PMC_SPLIT_MT
-        if (sflag(mt)) {
-            histogram_mt(ntok, len);
-            return;
-        }
-#endif
         const int l = lane_id();
         const Tables &TT = c_tables;
         for (int s = l; s < 352; s += 64) lfreq[s] = 0;
@@ -2223,86 +1875,6 @@ struct SmallWave {
         }
         if (l == 0) lfreq[kEndBlock] = 1;
         wave_sync();
-    }
-    // covered bits [s + skip, s + L) of every match record in the bitmap cov (lds_or per 32-bit word)
-    __device__ void cover_bits(PMC_LDS uint32_t *cov, PMC_LDS uint32_t *starts, uint32_t nm, uint32_t skip) {
-        for (uint32_t t = (uint32_t)lane_id(); t < nm; t += 64) {
-            const uint32_t r = tok[t], st = r >> 18;
-            uint32_t x = st + skip, e = st + (r & 0xffu) + 3u;
-            if (starts) lds_or(&starts[st >> 5], 1u << (st & 31));
-            while (x < e) {
-                const uint32_t b0 = x & 31, n = e - x < 32 - b0 ? e - x : 32 - b0;
-                lds_or(&cov[x >> 5], (n == 32 ? ~0u : (1u << n) - 1u) << b0);
-                x += n;
-            }
-        }
-    }
-    // histogram_mt: the match records' length / distance symbols, and the literal bytes at the
-    // positions no match covers (coverage bitmap in the front's X region, dead after the parse)
-    __device__ void histogram_mt(uint32_t nm, uint32_t len) {
-        const int l = lane_id();
-        PMC_LDS uint32_t *cov = (PMC_LDS uint32_t *)HC;
-        for (int s = l; s < 352; s += 64) lfreq[s] = 0;
-        for (uint32_t k = (uint32_t)l; k < (len + 31) / 32; k += 64) cov[k] = 0;
-        wave_sync();
-        for (uint32_t t = (uint32_t)l; t < nm; t += 64) {
-            const uint32_t r = tok[t];
-            lds_add(&lfreq[len_code_cf(r & 0xffu) + kLiterals + 1], 1u);
-            lds_add(&dfreq[dist_code_cf((r >> 8) & 1023u)], 1u);
-        }
-        cover_bits(cov, nullptr, nm, 0);
-        wave_sync();
-        for (uint32_t p = (uint32_t)l; p < len; p += 64)
-            if (!((cov[p >> 5] >> (p & 31)) & 1u)) lds_add(&lfreq[b[p]], 1u);
-        if (l == 0) lfreq[kEndBlock] = 1;
-        wave_sync();
-    }
-    // emit_symbols over positions (PMC_SPLIT_MT): a literal where no match covers, a match at a record's
-    // start (its record: the starts before it, counted in the start bitmap), nothing inside a match
-    __device__ uint64_t emit_symbols_mt(uint32_t nm, uint32_t len, uint64_t bitpos) {
-        const int l = lane_id();
-        PMC_LDS uint32_t *stb = (PMC_LDS uint32_t *)runs, *cov = stb + 32; // (runs is dead after the headers)
-        stb[l] = 0;
-        wave_sync();
-        cover_bits(cov, stb, nm, 1);
-        wave_sync();
-        uint32_t base = 0;
-        const uint64_t below = (1ull << l) - 1ull;
-        for (uint32_t c0 = 0; c0 < len; c0 += 64) {
-            const uint32_t p = c0 + (uint32_t)l, w = c0 >> 5;
-            const uint64_t sm = (uint64_t)stb[w] | (uint64_t)stb[w + 1] << 32;
-            const uint64_t cm = (uint64_t)cov[w] | (uint64_t)cov[w + 1] << 32;
-            uint32_t nb = 0;
-            uint64_t v = 0;
-            if (p < len) {
-                if ((sm >> l) & 1u) {
-                    const uint32_t r = tok[base + (uint32_t)__builtin_popcountll(sm & below)];
-                    const uint32_t lc = r & 0xffu, code = len_code_cf(lc);
-                    uint32_t c = lcode[code + kLiterals + 1];
-                    v = c & 0xffff;
-                    nb = c >> 16;
-                    const uint32_t xl = len_extra_cf(code);
-                    v |= (uint64_t)((lc - len_base_cf(code)) & ((1u << xl) - 1)) << nb;
-                    nb += xl;
-                    const uint32_t dm = (r >> 8) & 1023u, dc = dist_code_cf(dm);
-                    c = dcode[dc];
-                    v |= (uint64_t)(c & 0xffff) << nb;
-                    nb += c >> 16;
-                    const uint32_t xd = dist_extra_cf(dc);
-                    v |= (uint64_t)((dm - dist_base_cf(dc)) & ((1u << xd) - 1)) << nb;
-                    nb += xd;
-                } else if (!((cm >> l) & 1u)) {
-                    const uint32_t c = lcode[b[p]];
-                    v = c & 0xffff;
-                    nb = c >> 16;
-                }
-            }
-            const uint32_t incl = wave_incl_scan_dpp(nb);
-            if (nb) or_bits_lds(bitpos + incl - nb, v, (int)nb);
-            bitpos += readlane(incl, 63);
-            base += (uint32_t)__builtin_popcountll(sm);
-        }
-        return bitpos;
     }
     // gen_codes (trees.c) for code lengths Ls[0..elems): canonical code = next_code[len] +
     // rank among equal lengths; code_out[s] = bit-reversed code | len << 16 (0: unused)
@@ -2539,11 +2111,7 @@ struct SmallWave {
             wave_sync();
             PMC_STOP(24, bitpos)
         }
-#if PMC_SPLIT_MT
-        bitpos = sflag(mt) ? emit_symbols_mt(ntok, len, bitpos) : emit_symbols(ntok, bitpos);
-#else
         bitpos = emit_symbols(ntok, bitpos);
-#endif
         const uint32_t eob = lcode[kEndBlock];
         wave_sync();
         if (l == 0) or_bits_lds(bitpos, eob & 0xffff, (int)(eob >> 16));
@@ -2612,12 +2180,7 @@ struct SmallWave {
         const uint32_t npos = len >= 3 ? len - 2 : 0;
         uint32_t ntok;
         if (npos) {
-#if PMC_SORT_REG
-            const uint32_t k0 = cnp == 6 && npos > 512 ? sort_rank_reg<16, 6>(npos)
-                                                       : sort_positions2(npos, (PMC_LDS uint32_t *)CN);
-#else
             const uint32_t k0 = sort_positions2(npos, (PMC_LDS uint32_t *)CN);
-#endif
             stamp(1);
             PMC_STOP(12, 0)
             ntok = cnp == 6   ? parse_ondemand<6>(npos, len, k0)
@@ -2627,13 +2190,8 @@ struct SmallWave {
             PMC_STOP(14, 0)
             if (sflag(ntok == kNtokRetry ? 1u : 0u)) return kNtokRetry; // (sort guard: no histogram)
         } else {
-#if PMC_SPLIT_MT // (no match, no record)
-            if (!mt) lit_run(0, 0, len);
-            ntok = mt ? 0u : len;
-#else
             lit_run(0, 0, len);
             ntok = len;
-#endif
         }
         wave_sync_global();
         stamp(2);

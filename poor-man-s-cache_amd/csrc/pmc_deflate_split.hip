@@ -28,8 +28,8 @@ namespace pmc {
 // interleaved by 64-value block (lane-coalesced).
 
 // ---- front -------------------------------------------------------------------------------------
-// (8 waves per SIMD with PMC_FRONT_S10: the packed S leaves room for them at <= 1 KiB; 7 otherwise)
-__global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kernel(DeflateArgs a) {
+// (7 waves per SIMD: 72 VGPRs; 28 resident waves per CU at 1 KiB, which the LDS also allows)
+__global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
     uint8_t *base = lds + (uint64_t)wib * a.wave_bytes;
@@ -43,12 +43,6 @@ __global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kern
     w.HC = to_lds<uint64_t>(base + F.hc);
     w.EV = to_lds<uint32_t>(base + F.ev);
     w.cnp = F.pkb;
-#if PMC_FRONT_S10
-    w.s10 = front_s10(a.cap_len) ? 1u : 0u;
-#endif
-#if PMC_SPLIT_MT
-    w.mt = split_mt(a.cap_len) ? 1u : 0u;
-#endif
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;
@@ -101,11 +95,6 @@ __global__ void __launch_bounds__(256, PMC_FRONT_S10 ? 8 : 7) deflate_front_kern
 }
 
 // ---- trees (one lane per value) ------------------------------------------------------------------
-// PMC_TREES_SKIP: the per-lane symbol loops pass over unused symbols eight at a time (leaf insertion:
-// an all-zero 16-byte group of frequencies; scan_tree: the zero lengths that follow inside a zero run)
-#ifndef PMC_TREES_SKIP
-#define PMC_TREES_SKIP 0
-#endif
 // (RegU16, pmc_device.hpp: round 5 moved bl_count and the bit-length frequencies from the lane's LDS column
 // into registers, which with the 79-entry heap of the <= 1 KiB instance takes the kernel from 6 to 8 waves
 // per CU: it is LDS-bound and waits on its heap's dependent LDS round trips.  Per-lane VALU is cheap here:
@@ -183,10 +172,6 @@ struct LaneTrees {
                 }
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-#if PMC_TREES_SKIP
-                    // (eight unused symbols at once: a JSON value uses none of 0..31 and 127..255)
-                    if ((cur[i].x | cur[i].y | cur[i].z | cur[i].w) == 0u) continue;
-#endif
 #pragma unroll
                     for (int h = 0; h < 8; h++) {
                         const int nn = b * 32 + i * 8 + h;
@@ -370,19 +355,6 @@ struct LaneTrees {
                 nextlen = 0xffff;
             }
             if (++count < max_count && curlen == nextlen) {
-#if PMC_TREES_SKIP
-                // inside a run of zero lengths, the zero bytes after nextlen in the staged word are
-                // iterations that only count (each would take this branch): take them at once
-                if (curlen == 0 && nx - w0 < 7) {
-                    const uint64_t rest = pk >> (8 * (nx - w0 + 1));
-                    uint32_t k = rest ? (uint32_t)__builtin_ctzll(rest) >> 3 : (uint32_t)(7 - (nx - w0));
-                    const uint32_t lim_code = (uint32_t)(max_code - nx), lim_cnt = (uint32_t)(max_count - 1 - count);
-                    k = k < lim_code ? k : lim_code;
-                    k = k < lim_cnt ? k : lim_cnt;
-                    n += (int)k;
-                    count += (int)k;
-                }
-#endif
                 continue;
             }
             if (count < min_count) {
@@ -509,9 +481,6 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
     w.runs = to_lds<uint16_t>(base + B.runs);
     w.blfreq = to_lds<uint32_t>(base + B.blfreq);
     w.perm = to_lds<uint16_t>(base + B.perm);
-#if PMC_SPLIT_MT
-    w.mt = split_mt(a.cap_len) ? 1u : 0u; // (runs holds emit_symbols_mt's bitmaps after the headers)
-#endif
     // (run_back touches only the arrays above; the rest of w still points into the larger
     // small_layout and must stay unused here)
     PMC_LDS uint8_t *Ls = to_lds<uint8_t>(base + B.ls); // code lengths from the trees kernel

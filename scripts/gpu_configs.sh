@@ -1,9 +1,10 @@
 #!/bin/bash
 # Every BASELINE size plus the large values (30 KB, 64 KiB, 1 MiB) on the current kernels, with the
-# reference digest match of each leg (fullsize_parity; round 5: the large legs have digests too).
+# reference digest match of each leg (fullsize_parity).  Stops at the first failure.
+#   TAG=r6cfg bash scripts/gpu_configs.sh
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-T=${TAG:-r5cfg}
+T=${TAG:-cfg}
 mkdir -p gpurun_out/$T
 run() { # name, args...
   local name=$1; shift
