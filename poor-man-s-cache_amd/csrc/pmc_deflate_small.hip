@@ -949,7 +949,7 @@ struct SmallWave {
         cn = x < npos ? cn : 0u;
         cn1 = x + 1 < npos ? cn1 : 0u;
         const uint32_t w0 = SAT && cn == CMAX ? kPreCand : cn < kPreCand ? cn : kPreCand;
-        const uint32_t w = w0;
+        const uint32_t w = w0; // lanes of this position
         const uint32_t incl = wave_incl_scan_dpp(w), offs = incl - w;
         const bool inc = w != 0 && incl <= 64;
         const uint64_t im = ballot(inc); // evaluated (lane-owning) offsets
@@ -969,7 +969,7 @@ struct SmallWave {
         const bool v = l < nl;
         const uint32_t sc = wave_incl_max_dpp(mk);
         const uint32_t own = v ? ((sc >> 19) & 127) - 1 : 0u;
-        const uint32_t P = p0 + own, d = l - (sc >> 26) + 1;
+        const uint32_t P = p0 + own, d = l - (sc >> 26) + 1; // the lane's candidate: the d-th nearest
         const uint32_t rxo = sc & 0xffffu;
         uint32_t q = sget<PK>(v && (!SAT || rxo >= d) ? rxo - d : 0u);
         uint64_t A0, A1, B0, B1;
