@@ -315,6 +315,13 @@ int pmc_ctx_guard_counts(pmc_ctx *ctx, uint32_t counts[5]);
  * counted here.) */
 int pmc_ctx_path_counts(pmc_ctx *ctx, uint64_t counts[4]);
 
+/* Latency-path compress calls whose declined values were redone (build-owned).  The latency path's
+ * one kernel has no retry pass of its own: a value it declines (a lane-order guard fired, see
+ * pmc_ctx_guard_counts) is compressed again, alone with the call's other declined values, by a
+ * throughput-pipeline call into the caller's buffers (which also counts in counts[2] above).
+ * *n = the number of latency-path calls that needed that.  Host-side, no device synchronization. */
+int pmc_ctx_latency_redone(pmc_ctx *ctx, uint64_t *n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,6 +19,8 @@
 #include <string>
 #include <thread>
 
+#include <unistd.h>
+
 #include "../../include/pmc_codec.h"
 #include "pmc_device.hpp"
 #include "pmc_kernels.hpp"
@@ -185,6 +187,7 @@ struct pmc_ctx {
     // host-call routing (pmc_ctx_path_counts): [0] / [1] compress / decompress calls on the latency
     // path, [2] / [3] on the throughput pipeline
     uint64_t path_calls[4] = {0, 0, 0, 0};
+    uint64_t latency_redone = 0; // latency-path compress calls whose declined values a pipeline call redid
     // large values (pmc_deflate_large.hip): selection list, round tables, round scratch, emit scratch
     DevBuf lvsel, lvtab, lvbuf, lvemit;
     HostBuf lvpin;
@@ -414,6 +417,13 @@ PMC_API int pmc_ctx_path_counts(pmc_ctx *ctx, uint64_t counts[4]) {
     if (!ctx || !counts) return PMC_E_ARG;
     std::lock_guard<std::mutex> lock(ctx->host_mu);
     for (int k = 0; k < 4; k++) counts[k] = ctx->path_calls[k];
+    return PMC_OK;
+}
+
+PMC_API int pmc_ctx_latency_redone(pmc_ctx *ctx, uint64_t *n) {
+    if (!ctx || !n) return PMC_E_ARG;
+    std::lock_guard<std::mutex> lock(ctx->host_mu);
+    *n = ctx->latency_redone;
     return PMC_OK;
 }
 
@@ -723,7 +733,14 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
         // when there are none): at 2 waves per CU (round 1-2) the latency-bound walk left 64 KiB values
         // at 0.52 GiB/s, and a 64-wave retry pass left periodic 1 MiB values and multi-block 24 KB
         // values 32x short of that
-        hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ctx->cus * 8,
+        // A batch of single-block values (max_len <= kSmallMax) can have retries only from a lane-order
+        // guard, which never fired on gfx950 (and a context whose create-time probe sees the order broken
+        // sends every batch to the per-lane-counter kernels instead): 64 waves, and 64 waves' scratch,
+        // cover that.  Only batches with longer values (multi-block large-pass values, large values whose
+        // segments did not stitch) size the pass for throughput (the scratch a gated pass
+        // allocates stays with the context).
+        const uint64_t cap_waves = gated && max_len <= kSmallMax ? 64ull : (uint64_t)ctx->cus * 8;
+        hbm_waves = std::max<uint64_t>(1, std::min<uint64_t>(cap_waves,
                                                              ((gated ? 8ull : 32ull) << 30) / std::max<uint64_t>(hbm_wb, 1)));
     }
     hbm_waves = std::min<uint64_t>(hbm_waves, n);
@@ -1102,7 +1119,10 @@ PMC_API int pmc_gzip_decompress_batch(pmc_ctx *ctx, const uint8_t *src, const ui
     // A batch of at most 4 members per CU also takes the wave kernels whatever its sizes: one wave per
     // member beats one lane per member until the lanes' density pays (1000 x 1 MiB: 220 ms against 453 ms
     // through the multi-block lane pass; 40K x 64 KiB: 542 ms against 25 ms -- round 5, same box).
-    const bool small = latency_decompress(n, max_len, (uint64_t)n * max_len) || (uint64_t)n <= 4ull * ctx->cus;
+    // (PMC_LATENCY_BATCH=0 turns both clauses off, so A/B runs and fault tests can still reach the lane /
+    // record pipeline with small batches -- ADVICE r5)
+    const bool small = latency_decompress(n, max_len, (uint64_t)n * max_len) ||
+                       (latency_batch() != 0 && (uint64_t)n <= 4ull * ctx->cus);
     r = decompress_batch_body(ctx, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, max_len, stream, small,
                               true);
     const int r2 = dir_leave(ctx, 1, st);
@@ -1183,11 +1203,14 @@ class CopyPool {
     // runs part(k) for k = 0 .. t - 1 (t <= parts()), part 0 on the calling thread
     template <class F>
     void run(unsigned t, F part) {
-        if (t <= 1) {
-            part(0u);
+        // Inline on the calling thread when: one part; a process forked after the pool started (the child
+        // has no workers); or the pool is busy with another context's copies (a server's SET and
+        // GET contexts copy at the same time: the second caller does its own copies instead of waiting).
+        std::unique_lock<std::mutex> one(run_mu, std::defer_lock);
+        if (t <= 1 || getpid() != owner || !one.try_lock()) {
+            for (unsigned k = 0; k < t; k++) part(k);
             return;
         }
-        std::lock_guard<std::mutex> one(run_mu); // (calls from several contexts' threads take turns)
         std::unique_lock<std::mutex> lk(mu);
         fn = [&part](unsigned k) { part(k); };
         want = t - 1;
@@ -1203,7 +1226,7 @@ class CopyPool {
     }
 
   private:
-    CopyPool() {
+    CopyPool() : owner(getpid()) {
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         const unsigned cap = getenv("PMC_HOST_THREADS") ? (unsigned)std::max(1, atoi(getenv("PMC_HOST_THREADS")))
                                                         : std::min(8u, hw);
@@ -1224,6 +1247,7 @@ class CopyPool {
             if (--left == 0) done.notify_one();
         }
     }
+    const pid_t owner; // the process whose threads these workers are
     std::mutex mu, run_mu;
     std::condition_variable cv, done;
     std::function<void(unsigned)> fn;
@@ -1245,15 +1269,14 @@ double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
-               uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
-               int32_t *rc) {
-    if (!ctx) return PMC_E_ARG;
+// (the caller holds ctx->host_mu; force_pipeline: the throughput route whatever the batch's size)
+int host_batch_locked(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+                      uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+                      int32_t *rc, bool force_pipeline) {
     if (n == 0) return PMC_OK;
     static const bool trace = getenv("PMC_HOST_TRACE") && atoi(getenv("PMC_HOST_TRACE"));
     double t[8] = {};
     if (trace) t[0] = now_us();
-    HostCall guard(ctx);
     HIP_TRY(hipSetDevice(ctx->device));
     // packed device layout, in the order of the two copies: [offsets, lengths, caps | source bytes]
     // go down in one H2D, [output lengths, verdicts | output bytes] come back in one D2H
@@ -1276,8 +1299,8 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     // pipeline); its batch limit is 4,096 members / 16 MiB of output (latency_decompress:
     // round 5 measured the wave kernel still 2x ahead there).
     const uint64_t lat_max = latency_max_len(), lat_batch = latency_batch();
-    const bool latency = dir == kCompress ? n <= lat_batch && max_len <= lat_max
-                                          : latency_decompress(n, max_len, out_bytes);
+    const bool latency = !force_pipeline && (dir == kCompress ? n <= lat_batch && max_len <= lat_max
+                                                              : latency_decompress(n, max_len, out_bytes));
     ctx->path_calls[(latency ? 0 : 2) + (dir == kCompress ? 0 : 1)]++;
     // The latency path's kernel reads its inputs from, and writes its outputs to, coherent host memory in
     // place: no H2D / D2H copies (each a runtime copy kernel of its own) around its one launch.
@@ -1362,17 +1385,33 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     if (trace) t[2] = now_us();
     if (!zc) HIP_TRY(hipMemcpyAsync(h_dlen, d_dlen, up, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (zc && dir == kCompress) {
-        // the latency path launches no retry pass: a value its kernel declined (a lane-order guard fired)
-        // sends the call through the pipeline, whose gated HBM pass redoes it
-        bool again = false;
-        for (uint32_t i = 0; i < n && !again; i++) again = h_rc[i] == kDeflateRetry;
-        if (again) {
-            if ((r = run(false))) {
-                (void)hipStreamSynchronize(st);
-                return r;
-            }
-            HIP_TRY(hipStreamSynchronize(st));
+    // The latency path launches no retry pass: the values its kernel declined (a lane-order guard fired)
+    // are redone, alone, by a pipeline call (its gated HBM pass), straight into the caller's buffers.
+    std::vector<uint32_t> redo;
+    if (zc && dir == kCompress)
+        for (uint32_t i = 0; i < n; i++)
+            if (h_rc[i] == kDeflateRetry) redo.push_back(i);
+    std::vector<uint8_t> redone(redo.empty() ? 0 : n, 0);
+    if (!redo.empty()) {
+        ctx->latency_redone++;
+        const uint32_t m = (uint32_t)redo.size();
+        std::vector<uint64_t> r_soff(m), r_doff(m);
+        std::vector<uint32_t> r_slen(m), r_cap(m), r_dlen(m);
+        std::vector<int32_t> r_rc(m);
+        for (uint32_t k = 0; k < m; k++) {
+            const uint32_t i = redo[k];
+            r_soff[k] = src_off[i];
+            r_slen[k] = src_len[i];
+            r_cap[k] = dst_cap[i];
+            r_doff[k] = dst_off ? dst_off[i] : h_doff[i];
+            redone[i] = 1;
+        }
+        if ((r = host_batch_locked(ctx, dir, src, r_soff.data(), r_slen.data(), m, dst, r_doff.data(), r_cap.data(),
+                                   r_dlen.data(), r_rc.data(), true)))
+            return r;
+        for (uint32_t k = 0; k < m; k++) {
+            h_rc[redo[k]] = r_rc[k];
+            h_dlen[redo[k]] = r_dlen[k];
         }
     }
     if (trace) t[3] = now_us();
@@ -1380,10 +1419,10 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
     for (uint32_t i = 0; i < n; i++) {
         rc[i] = h_rc[i];
         dst_len[i] = h_dlen[i];
-        if (h_rc[i] == 0) moved += h_dlen[i];
+        if (h_rc[i] == 0 && (redone.empty() || !redone[i])) moved += h_dlen[i];
     }
     par_values(n, moved, [&](uint32_t i) {
-        if (h_rc[i] != 0) return;
+        if (h_rc[i] != 0 || (!redone.empty() && redone[i])) return; // (redone values are in place already)
         uint64_t to = dst_off ? dst_off[i] : h_doff[i];
         memcpy(dst + to, h_dst + h_doff[i], h_dlen[i]);
     });
@@ -1397,6 +1436,15 @@ int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_of
                 t[4] - t[3], t[4] - t[0]);
     }
     return PMC_OK;
+}
+
+int host_batch(pmc_ctx *ctx, Dir dir, const uint8_t *src, const uint64_t *src_off, const uint32_t *src_len,
+               uint32_t n, uint8_t *dst, const uint64_t *dst_off, const uint32_t *dst_cap, uint32_t *dst_len,
+               int32_t *rc) {
+    if (!ctx) return PMC_E_ARG;
+    if (n == 0) return PMC_OK;
+    HostCall guard(ctx);
+    return host_batch_locked(ctx, dir, src, src_off, src_len, n, dst, dst_off, dst_cap, dst_len, rc, false);
 }
 
 // Rebases one chunk's offsets onto its device copy: src_off -= sb, dst_off -= db (dst_off may be null).

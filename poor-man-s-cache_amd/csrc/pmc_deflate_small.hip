@@ -119,12 +119,22 @@ struct FrontLayout {
     int pkb;             // chain-count bits packed into R's top (front_pkb), 0: CN array, -1: HC only
     uint64_t cn, hc, ev; // parse scratch in X (cn unused when pk); the sort's 512-B table at X
 };
+// PMC_FRONT_S12: at 3-4 KiB (pkb 4, positions < 4096) the sorted positions are packed as 12-bit fields
+// (8 per 3 dwords, 4 spare bytes for the read of the last field's next dword): the front's LDS per wave
+// drops from 21.4 to 19.3 KB, so a CU holds 8 waves instead of 7 (round 2 measured 6 -> 7 waves as
+// 256 -> 244 ms at 4 KiB).
+#ifndef PMC_FRONT_S12
+#define PMC_FRONT_S12 1
+#endif
+__host__ __device__ inline bool front_s12(uint64_t n) { return PMC_FRONT_S12 && front_pkb(n) == 4; }
 __host__ __device__ inline FrontLayout front_layout(uint64_t n) {
     auto a = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
     FrontLayout F;
     F.bytes = 0;
     F.S = a(n + 32);
-    F.R = F.S + a(2 * n + 2);
+    // (the packed S keeps >= 256 B: the sort parks its 128 high-digit counters there)
+    const uint64_t s_bytes = front_s12(n) ? ((n * 12 + 31) / 32) * 4 + 4 : 2 * n + 2;
+    F.R = F.S + a(s_bytes > 256 ? s_bytes : 256);
     F.X = F.R + a(2 * n + 2);
     F.pkb = front_pkb(n);
     F.cn = F.X;
@@ -303,6 +313,7 @@ struct SmallWave {
     PMC_LDS uint8_t *b;
     PMC_LDS uint32_t *bw;
     PMC_LDS uint16_t *S, *R;
+    uint32_t s12 = 0; // front at 3-4 KiB (front_s12): S packed as 12-bit fields (sget<4>)
     PMC_LDS uint32_t *lfreq, *dfreq, *blfreq;
     PMC_LDS uint32_t *outw;
     PMC_LDS uint8_t *outb;
@@ -350,10 +361,16 @@ struct SmallWave {
 #define PMC_STOP(k, ret)
 #endif
 
-    // sorted position k
+    // sorted position k: u16, or (PK 4 with PMC_FRONT_S12) bits 12 k .. 12 k + 11 of the packed words
     template <int PK>
     __device__ __forceinline__ uint32_t sget(uint32_t k) const {
-        return S[k];
+        if constexpr (PK == 4 && PMC_FRONT_S12) {
+            PMC_LDS const uint32_t *S32 = (PMC_LDS const uint32_t *)S;
+            const uint32_t bit = 12u * k, w = bit >> 5;
+            return __builtin_amdgcn_alignbit(S32[w + 1], S32[w], bit & 31u) & 0xfffu;
+        } else {
+            return S[k];
+        }
     }
     __device__ uint32_t load4(uint32_t p) const {
         uint32_t w0 = bw[p >> 2], w1 = bw[(p >> 2) + 1];
@@ -539,6 +556,10 @@ struct SmallWave {
                 scan_tab();
                 wave_sync();
             }
+            if ((uint32_t)pass & s12) { // (packed S: the scatter ORs 12-bit fields into zeroed words)
+                for (uint32_t k = l; k < (npos * 12 + 31) / 32 + 1; k += 64) ((PMC_LDS uint32_t *)S)[k] = 0u;
+                wave_sync();
+            }
             // a lane's slot from one returning LDS atomic on its digit's counter: the lanes of one
             // ds_add_rtn to a word get their old values in lane order (scripts/micro/
             // lds_atomic_order.hip: 16.7M trials of skewed digit mixes, none out of order), so the
@@ -553,7 +574,13 @@ struct SmallWave {
                 const uint32_t d = (hash3(load4(p)) >> sh) & 255, hs = 16 * (d & 1);
                 if (x < npos) {
                     const uint32_t slot = (lds_add(&tab[d >> 1], 1u << hs) >> hs) & 0xffffu;
-                    dst[slot] = (uint16_t)p;
+                    if ((uint32_t)pass & s12) {
+                        const uint32_t bit = 12u * slot, w = bit >> 5, bs = bit & 31u;
+                        lds_or((PMC_LDS uint32_t *)S + w, p << bs);
+                        if (bs > 20u) lds_or((PMC_LDS uint32_t *)S + w + 1, p >> (32u - bs));
+                    } else {
+                        dst[slot] = (uint16_t)p;
+                    }
                 }
             }
             wave_sync();
@@ -2426,7 +2453,13 @@ __global__ void __launch_bounds__(256, 4) deflate_small_kernel(DeflateArgs a) {
                 }
                 continue;
             }
+#ifdef PMC_FAULT_LANE_ORDER // (diagnostic build: this kernel's sort and code ranks need no lane order, so it
+                            // declines every odd value itself, as a guard would: the retry routes get exercised)
+            int rc = (v & 1) ? kDeflateRetry
+                             : w.run(a.src + a.src_off[v], len, a.dst + a.dst_off[v], a.dst_cap[v], a.dst_len + v);
+#else
             int rc = w.run(a.src + a.src_off[v], len, a.dst + a.dst_off[v], a.dst_cap[v], a.dst_len + v);
+#endif
             if (l == 0) {
                 a.rc[v] = rc;
                 if (rc) a.dst_len[v] = 0;

@@ -43,6 +43,7 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     w.HC = to_lds<uint64_t>(base + F.hc);
     w.EV = to_lds<uint32_t>(base + F.ev);
     w.cnp = F.pkb;
+    w.s12 = front_s12(a.cap_len) ? 1u : 0u;
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;

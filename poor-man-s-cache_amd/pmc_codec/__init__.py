@@ -90,6 +90,7 @@ SIGNATURES = {
     "pmc_ctx_kernel_times": (_c.c_int, [_p, _c.POINTER(_c.c_double), _c.POINTER(_u32), _c.c_int]),
     "pmc_ctx_guard_counts": (_c.c_int, [_p, _c.POINTER(_u32)]),
     "pmc_ctx_path_counts": (_c.c_int, [_p, _c.POINTER(_u64)]),
+    "pmc_ctx_latency_redone": (_c.c_int, [_p, _c.POINTER(_u64)]),
 }
 
 # pmc_ctx_kernel_times kinds (include/pmc_codec.h PMC_K_*)
@@ -206,6 +207,15 @@ class Context:
             raise CodecUnavailable(f"pmc_ctx_path_counts failed ({rc})")
         return {"latency_compress": c[0], "latency_decompress": c[1], "pipeline_compress": c[2],
                 "pipeline_decompress": c[3]}
+
+    def latency_redone(self):
+        """Latency-path compress calls whose declined values a pipeline call redid (include/pmc_codec.h
+        pmc_ctx_latency_redone)."""
+        c = _u64(0)
+        rc = lib().pmc_ctx_latency_redone(self.handle, ctypes.byref(c))
+        if rc != 0:
+            raise CodecUnavailable(f"pmc_ctx_latency_redone failed ({rc})")
+        return c.value
 
     def close(self):
         if self.handle:

