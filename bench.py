@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--mix-keys", type=int, default=1_000_000)
     ap.add_argument("--mix-serial", action="store_true", help="SETs and GETs of a batch on one stream")
     ap.add_argument("--mix-ops", type=int, default=1_048_576)
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05", "traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06", "traffic.json"),
                     help="PMC-derived HBM bytes and issue counters per launch (scripts/pmc_traffic.py); used "
                          "only if its source_id matches the library's sources")
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-core CPU baseline "

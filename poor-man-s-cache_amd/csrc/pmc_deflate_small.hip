@@ -457,7 +457,8 @@ struct SmallWave {
         // address, so fewer lanes of a returning atomic serialise on one word): the 256 low-digit
         // counters in S (free until the second scatter), the 128 high-digit ones in tab
         // (values of 512 .. 1024 bytes: S then spans at least 1 KiB, the cap's 2 * cap + 2 bytes)
-        if (npos >= 510 && npos <= 1022) {
+        // (not with a packed S: this path's second scatter writes u16 entries)
+        if (npos >= 510 && npos <= 1022 && !s12) {
             PMC_LDS uint32_t *cl = (PMC_LDS uint32_t *)S;
             for (uint32_t k = l; k < 256; k += 64) cl[k] = 0;
             for (uint32_t k = l; k < 128; k += 64) tab[k] = 0;
