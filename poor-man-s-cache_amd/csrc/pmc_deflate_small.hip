@@ -993,7 +993,11 @@ struct SmallWave {
         wave_sync();
         const uint32_t mk = EV[l];
         // (LDS keeps one wave's accesses in order: the read above sees the marks)
-        EV[l] = 0;
+        // Values of <= 4 KiB (PK > 0 always) take each offset's maximum by the segmented max-scan below,
+        // which stores every evaluated offset's word: no reset for them (a non-evaluated offset's word is
+        // never read: its walk masks come from the counts).  The atomic-max path needs zeros.
+        constexpr bool kSegOnly = PK > 0;
+        if (!kSegOnly) EV[l] = 0;
         const bool v = l < nl;
         const uint32_t sc = wave_incl_max_dpp(mk);
         const uint32_t own = v ? ((sc >> 19) & 127) - 1 : 0u;
@@ -1035,7 +1039,7 @@ struct SmallWave {
             off += 16;
         }
         cl = cl < nice ? cl : nice;
-        if (sflag(len <= 4096 ? 1u : 0u)) {
+        if (kSegOnly || sflag(len <= 4096 ? 1u : 0u)) {
             // An offset's lanes are contiguous and own grows with the lane: an inclusive max-scan of
             // own << 26 | (cl, nearness, q) leaves each offset's maximum in its last lane, which stores it.
             // No same-address LDS atomics: the lanes of one position used to serialise on its word (round 4:
