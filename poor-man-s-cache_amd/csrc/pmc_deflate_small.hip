@@ -299,6 +299,15 @@ struct TreeOut {
 // chain candidates evaluated per position by the on-demand parse's wave step (the rest, when
 // needed, by search()); at most 32 (5-bit field in the eval key)
 constexpr uint32_t kPreCandLanes = 32;
+// PMC_EVAL_BPERM: each eval offset fetches its position's maximum from the position's last lane by
+// ds_bpermute instead of an LDS store by that lane and a read back
+#ifndef PMC_EVAL_BPERM
+#define PMC_EVAL_BPERM 1
+#endif
+// PMC_EVAL_CN1DPP: the eval's count of position x + 1 by a DPP move from lane l + 1
+#ifndef PMC_EVAL_CN1DPP
+#define PMC_EVAL_CN1DPP 1
+#endif
 // A uniform 0/1 integer the compiler may not turn back into a bool: branching on it is one
 // s_cmp + s_cbranch_scc.  (Bools merged across blocks become 64-bit lane masks -- s_cselect_b64,
 // s_and_b64 with exec, s_cbranch_vcc -- on the scalar unit, which the parse saturates.)
@@ -966,16 +975,23 @@ struct SmallWave {
         if (PK > 0) {
             cn = rx >> RB;
             rx &= (1u << RB) - 1u;
-            cn1 = (uint32_t)R[x1] >> RB;
         } else if (PK < 0) { // (no counts: 1 = has candidates, SAT)
             cn = (uint32_t)(HC[xc >> 6] >> (xc & 63)) & 1u;
-            cn1 = (uint32_t)(HC[x1 >> 6] >> (x1 & 63)) & 1u;
         } else {
             cn = CN[xc];
-            cn1 = CN[x1];
         }
         cn = x < npos ? cn : 0u;
+#if PMC_EVAL_CN1DPP
+        // x + 1's count is lane l + 1's (one DPP move instead of an LDS read).  Lane 63 takes 1 ("x + 1 has
+        // candidates"): offset 63 is then never a fast step, and the walk's general step decides it exactly.
+        cn1 = (uint32_t)__builtin_amdgcn_update_dpp(1, (int)cn, 0x130, 0xf, 0xf, false); // wave_shl:1
+        (void)x1;
+#else
+        if (PK > 0) cn1 = (uint32_t)R[x1] >> RB;
+        else if (PK < 0) cn1 = (uint32_t)(HC[x1 >> 6] >> (x1 & 63)) & 1u;
+        else cn1 = CN[x1];
         cn1 = x + 1 < npos ? cn1 : 0u;
+#endif
         const uint32_t w0 = SAT && cn == CMAX ? kPreCand : cn < kPreCand ? cn : kPreCand;
         const uint32_t w = w0; // lanes of this position
         const uint32_t incl = wave_incl_scan_dpp(w), offs = incl - w;
@@ -1039,24 +1055,37 @@ struct SmallWave {
             off += 16;
         }
         cl = cl < nice ? cl : nice;
+        uint32_t kk; // offset l's result: best << 23 | nearness << 18 | q
         if (kSegOnly || sflag(len <= 4096 ? 1u : 0u)) {
             // An offset's lanes are contiguous and own grows with the lane: an inclusive max-scan of
-            // own << 26 | (cl, nearness, q) leaves each offset's maximum in its last lane, which stores it.
+            // own << 26 | (cl, nearness, q) leaves each offset's maximum in its last lane.
             // No same-address LDS atomics: the lanes of one position used to serialise on its word (round 4:
             // front 194 -> 185 ms at 1 KiB).  Positions < 4096 at these sizes, so q takes 12 bits.
             const uint32_t k2 = own << 26 | (vk ? cl << 17 | (kPreCand - d) << 12 | q : 0u);
             const uint32_t mx = wave_incl_max_dpp(k2);
+#if PMC_EVAL_BPERM
+            // offset l reads its maximum from its last lane, incl - 1, by one ds_bpermute (no exec-masked
+            // store, wave sync and read back); an offset without lanes reads some lane's word, which nothing
+            // uses (its walk masks come from the counts)
+            const uint32_t m = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((incl - 1u) & 63u) << 2), (int)mx) &
+                               0x3ffffffu;
+            kk = (m >> 17) << 23 | ((m >> 12) & 31u) << 18 | (m & 4095u);
+#else
             const uint32_t onx = (uint32_t)__builtin_amdgcn_update_dpp(64, (int)own, 0x130, 0xf, 0xf, false); // lane l + 1
             if (v && (l + 1 >= nl || onx != own)) {
                 const uint32_t m = mx & 0x3ffffffu;
                 EV[own] = (m >> 17) << 23 | ((m >> 12) & 31u) << 18 | (m & 4095u);
             }
+            wave_sync();
+            kk = EV[l];
+#endif
         } else {
             __hip_atomic_fetch_max(&EV[own], vk ? cl << 23 | (kPreCand - d) << 18 | q : 0u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WAVEFRONT);
+            wave_sync();
+            kk = EV[l];
         }
-        wave_sync();
-        const uint32_t kk = EV[l], best = kk >> 23;
+        const uint32_t best = kk >> 23;
         const uint32_t nx = (len - x) < 258 ? (len - x) : 258;
         auto neg = [](uint32_t d) { return d >> 31; }; // 1 iff d < 0 as int (all values here are small)
         uint32_t cutc = (SAT ? (cn == CMAX ? 1u : 0u) : neg(kPreCand - cn)) & neg(best - nx);
