@@ -304,9 +304,20 @@ constexpr uint32_t kPreCandLanes = 32;
 #ifndef PMC_EVAL_BPERM
 #define PMC_EVAL_BPERM 1
 #endif
+// PMC_HC_FROM_R: with chain counts in R (PK > 0) the walk's has-candidate words are ballots of those
+// counts, so build_cn sets no HC bits (no same-word LDS atomics)
+#ifndef PMC_HC_FROM_R
+#define PMC_HC_FROM_R 1
+#endif
 // PMC_EVAL_CN1DPP: the eval's count of position x + 1 by a DPP move from lane l + 1
 #ifndef PMC_EVAL_CN1DPP
 #define PMC_EVAL_CN1DPP 1
+#endif
+// (the fault build runs the u32-counter sort's first scatter from the loop below, whose lanes it reverses)
+#ifdef PMC_FAULT_LANE_ORDER
+#define PMC_FAULT_PASS0 0
+#else
+#define PMC_FAULT_PASS0 1
 #endif
 // A uniform 0/1 integer the compiler may not turn back into a bool: branching on it is one
 // s_cmp + s_cbranch_scc.  (Bools merged across blocks become 64-bit lane masks -- s_cselect_b64,
@@ -475,9 +486,16 @@ struct SmallWave {
             auto agg_add = [&](PMC_LDS uint32_t *ctr, uint32_t d, bool valid) -> uint32_t {
                 return valid ? lds_add(&ctr[d], 1u) : 0u;
             };
-            for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
+            // (the hashes of positions c0 + l stay in registers, two per VGPR, for the first scatter, which
+            // visits the same positions in the same lanes: no second load4 of them)
+            uint32_t hreg[8];
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                const uint32_t c0 = 64u * (uint32_t)c;
+                if (c0 >= npos) break;
                 const uint32_t x = c0 + l;
                 const uint32_t h = hash3(load4(x < npos ? x : 0u));
+                hreg[c >> 1] = (c & 1) ? hreg[c >> 1] | h << 16 : h;
                 k0 += (uint32_t)__builtin_popcountll(ballot(x < npos && h < h0));
                 agg_add(cl, h & 255, x < npos);
                 agg_add(tab, (h >> 8) & 127, x < npos);
@@ -499,7 +517,18 @@ struct SmallWave {
                 tab[2 * l + 1] = hb + h0c;
             }
             wave_sync();
-            for (int pass = 0; pass < 2; pass++) {
+#ifndef PMC_FAULT_LANE_ORDER
+#pragma unroll
+            for (int c = 0; c < 16; c++) { // first scatter, by the low digit, into Tt
+                const uint32_t c0 = 64u * (uint32_t)c;
+                if (c0 >= npos) break;
+                const uint32_t x = c0 + l, h = (hreg[c >> 1] >> (16 * (c & 1))) & 0xffffu;
+                const uint32_t slot = agg_add(cl, h & 255, x < npos);
+                if (x < npos) Tt[slot] = (uint16_t)x;
+            }
+            wave_sync();
+#endif
+            for (int pass = PMC_FAULT_PASS0; pass < 2; pass++) {
                 PMC_LDS uint32_t *ctr = pass ? tab : cl;
                 PMC_LDS uint16_t *dst = pass ? S : Tt;
                 for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
@@ -892,14 +921,28 @@ struct SmallWave {
     // (measured on gfx950, not documented).  The guard checks what that order must produce -- (hash,
     // position) strictly increasing along S -- and the caller sends the value to the retry kernel
     // (per-lane counters, no atomic order) instead of parsing chains that may point forward.
+    // has-candidate bits of positions 64 w .. 64 w + 63 (uniform): with the counts in R (PK > 0) a ballot of
+    // them (one LDS read, as the HC word's), otherwise the HC word build_cn set
+    template <int PK>
+    __device__ __forceinline__ uint64_t hc_word(uint32_t w, uint32_t npos) const {
+        if constexpr (PK > 0 && PMC_HC_FROM_R) {
+            const uint32_t x = w * 64u + (uint32_t)lane_id();
+            return ballot(x < npos && (uint32_t)R[x < npos ? x : 0u] >> (16 - PK) != 0u);
+        } else {
+            return rfl64(HC[w]);
+        }
+    }
     template <int PK>
     __device__ __forceinline__ uint32_t build_cn(uint32_t npos, uint32_t k0) {
         constexpr uint32_t RB = 16 - (PK > 0 ? PK : 0), CMAX = PK > 0 ? (1u << PK) - 1 : 255u;
         const uint32_t l = (uint32_t)lane_id();
         // has-candidate bits set by position below (HC as u32 words, LDS atomics): no second
-        // pass over the positions
-        for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
-        wave_sync();
+        // pass over the positions.  (PK > 0: the walk takes them from R's counts, hc_word)
+        constexpr bool kHc = !(PK > 0 && PMC_HC_FROM_R);
+        if (kHc) {
+            for (uint32_t k = l; k < (npos + 63) / 64 * 2; k += 64) ((PMC_LDS uint32_t *)HC)[k] = 0u;
+            wave_sync();
+        }
         uint32_t ph = 0xffffffffu, prs = 0, pq = 0; // previous chunk's last hash, run start, position
         uint32_t bad = 0;
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
@@ -918,7 +961,7 @@ struct SmallWave {
             if (valid) { // (the rank array R is written here, not by the sort)
                 R[p] = (uint16_t)(PK > 0 ? k | (cnt < CMAX ? cnt : CMAX) << RB : k);
                 if (PK == 0) CN[p] = (uint8_t)(cnt < 255 ? cnt : 255);
-                if (cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
+                if (kHc && cnt) lds_or((PMC_LDS uint32_t *)HC + (p >> 5), 1u << (p & 31));
             }
             ph = readlane(h, 63);
             prs = readlane(rs, 63);
@@ -1217,7 +1260,7 @@ struct SmallWave {
         TokBuf tb;
         uint32_t i = 0, ml = 2, ms = 0, lf = 0; // lf: first position of the pending literal run
         uint32_t hci = 0;              // HC word cached in SGPRs
-        uint64_t hcw = rfl64(HC[0]);
+        uint64_t hcw = hc_word<PK>(0, npos);
 #ifdef PMC_STAMPS
         // eval usage (stamps build): st[3] evaluated positions, st[4] those the walk consumed,
         // st[5] evals started inside the previous window's 64-position span
@@ -1265,12 +1308,12 @@ struct SmallWave {
                         if (w < nw) {
                             if (w != hci) {
                                 hci = w;
-                                hcw = rfl64(HC[w]);
+                                hcw = hc_word<PK>(w, npos);
                             }
                             uint64_t m = hcw & (~0ull << (i & 63));
                             while (!m && ++w < nw) {
                                 hci = w;
-                                hcw = rfl64(HC[w]);
+                                hcw = hc_word<PK>(w, npos);
                                 m = hcw;
                             }
                             if (m) j = w * 64 + (uint32_t)__builtin_ctzll(m);
@@ -1318,7 +1361,7 @@ struct SmallWave {
             if (sflag((i < npos ? 1u : 0u) & (pl < 258 ? 1u : 0u))) {
                 if ((i >> 6) != hci) {
                     hci = i >> 6;
-                    hcw = rfl64(HC[hci]);
+                    hcw = hc_word<PK>(hci, npos);
                 }
                 if (sflag((uint32_t)(hcw >> (i & 63)) & 1u)) {
 #ifdef PMC_STAMPS
