@@ -2256,10 +2256,14 @@ struct SmallWave {
                     const v4u y = *(PMC_GLB const v4u *)(s16 + k);
                     x = make_uint4(y.x, y.y, y.z, y.w);
                 }
-                bw[4 * k] = x.x;
-                if (4 * k + 1 < nw) bw[4 * k + 1] = x.y;
-                if (4 * k + 2 < nw) bw[4 * k + 2] = x.z;
-                if (4 * k + 3 < nw) bw[4 * k + 3] = x.w;
+                if (4 * k + 3 < nw) { // (one 16-byte LDS store; the padded tail dword by dword)
+                    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                    *(PMC_LDS v4u *)(bw + 4 * k) = v4u{x.x, x.y, x.z, x.w};
+                } else {
+                    bw[4 * k] = x.x;
+                    if (4 * k + 1 < nw) bw[4 * k + 1] = x.y;
+                    if (4 * k + 2 < nw) bw[4 * k + 2] = x.z;
+                }
             }
             wave_sync();
             for (uint32_t k = full16 * 16 + l; k < len; k += 64) b[k] = src[k];

@@ -62,6 +62,12 @@ static_assert(kRecFlushAt >= 4 && kRecFlushAt <= kRecStage && kRecStage % 4 == 0
 #endif
 // PMC_REC_OUT1K: a batch whose outputs are all <= 1 KiB (dst_cap) runs the instance whose phase B
 // image holds 1 KiB (phase B's LDS then fits inside phase A's); others the 4 KiB image.
+// PMC_REC_DPOS: phase B keeps each record's match distance at the record's start position (in the
+// position array itself) instead of a per-record array indexed through a popcount of the start bitmap:
+// two 16-byte LDS reads per lane per 1,024 positions instead of sixteen u16 reads
+#ifndef PMC_REC_DPOS
+#define PMC_REC_DPOS 1
+#endif
 #ifndef PMC_REC_OUT1K
 #define PMC_REC_OUT1K 1
 #endif
@@ -107,8 +113,14 @@ struct RecB {
     static constexpr uint32_t kOut1 = kOut0 + OUT + 32;
     static constexpr uint32_t kSrc = kOut1 + OUT + 32;
     static constexpr uint32_t kBits = kSrc + 2 * OUT;
+#if PMC_REC_DPOS
+    // (a record's distance sits at its start position in the src array, written before the position round
+    // overwrites that position: no per-record array)
+    static constexpr uint32_t kEnd = kBits + OUT / 8;
+#else
     static constexpr uint32_t kRecD = kBits + OUT / 8;
     static constexpr uint32_t kEnd = kRecD + 2 * (OUT < kRecMax ? OUT : kRecMax); // (records <= output bytes)
+#endif
     static constexpr uint32_t kLds = kEnd > kRecALds ? kEnd : kRecALds;          // phase B reuses phase A's LDS
     static_assert(OUT % 1024 == 0, "positions resolve 1024 at a time");
 };
@@ -225,7 +237,9 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
     PMC_LDS uint8_t *ob0 = to_lds<uint8_t>(lds + B::kOut0), *ob1 = to_lds<uint8_t>(lds + B::kOut1);
     PMC_LDS uint16_t *srcv = to_lds<uint16_t>((uint16_t *)(lds + B::kSrc));
     PMC_LDS uint32_t *bits = to_lds<uint32_t>((uint32_t *)(lds + B::kBits));
+#if !PMC_REC_DPOS
     PMC_LDS uint16_t *recd = to_lds<uint16_t>((uint16_t *)(lds + B::kRecD));
+#endif
     const uint32_t rstride = a.rec_stride;
     PMC_GLB uint32_t *const rows = (PMC_GLB uint32_t *)a.rec_scratch + (uint64_t)blockIdx.x * 64 * rstride;
     PMC_GLB uint32_t *const row = rows + (uint64_t)lane * rstride;
@@ -528,7 +542,7 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                 const uint32_t ext = G == 1 ? osz[0] : 1024u; // image positions of the pass
                 for (uint32_t k = lane; k < (ext + 31) / 32; k += 64) bits[k] = 0;
                 wave_sync();
-                uint32_t R = 0;
+                uint32_t R = 0; // (records before this member's in the pass)
 #pragma unroll
                 for (int g = 0; g < G; g++) {
                     if (cm[g] < 0) continue;
@@ -546,7 +560,11 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                         if (k < mr) {
                             // a literal record places its bytes now; a match keeps its distance
                             const uint32_t nl = w >> 30;
+#if PMC_REC_DPOS
+                            srcv[s] = (uint16_t)(nl ? 0u : ((w >> 8) & 0x7fff) + 1); // (at the start position)
+#else
                             recd[R + k] = (uint16_t)(nl ? 0u : ((w >> 8) & 0x7fff) + 1);
+#endif
                             lds_or(&bits[s >> 5], 1u << (s & 31));
                             if (nl) ob[s] = (uint8_t)w;
                             if (nl >= 2) ob[s + 1] = (uint8_t)(w >> 8);
@@ -555,6 +573,7 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                         carry = rl(incl, 63);
                     }
                     R += mr;
+                    (void)R;
                 }
                 wave_sync();
                 // (b) the next pass's records; (c) the previous pass's images
@@ -562,7 +581,11 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                 if (nm[0] >= 0) fetch(nm);
                 flush_prev();
                 // (d) positions, 1024 per round (16 per lane): record, literal byte or source position
+#if PMC_REC_DPOS
+                uint32_t carry = 0; // (start position + 1) << 16 | distance of the last record start so far
+#else
                 uint32_t before = 0;
+#endif
                 for (uint32_t c0 = 0; c0 < ext; c0 += 1024) {
                     const uint32_t p0 = c0 + 16 * lane;
                     // end of the valid positions of the lane's member
@@ -575,11 +598,35 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                         lim += gl * span;
                     }
                     const uint32_t bw = p0 < lim ? (bits[p0 >> 5] >> (p0 & 16)) & 0xffffu : 0u;
+                    uint32_t sp[16];
+#if PMC_REC_DPOS
+                    // the distances at the lane's 16 positions (valid at record starts) in two 16-byte
+                    // reads, and the last start below the lane by a max-scan of (position, distance)
+                    uint32_t dv[8];
+                    {
+                        const rec_v4u d0 = *(PMC_LDS const rec_v4u *)(srcv + p0), d1 = *(PMC_LDS const rec_v4u *)(srcv + p0 + 8);
+                        dv[0] = d0.x, dv[1] = d0.y, dv[2] = d0.z, dv[3] = d0.w, dv[4] = d1.x, dv[5] = d1.y, dv[6] = d1.z, dv[7] = d1.w;
+                    }
+                    uint32_t dls = 0; // the distance at the lane's last start (a select chain: no indexed registers)
+#pragma unroll
+                    for (int i = 0; i < 16; i++) dls = (bw >> i) & 1u ? (dv[i >> 1] >> (16 * (i & 1))) & 0xffffu : dls;
+                    const uint32_t ls = bw ? 31u - (uint32_t)__builtin_clz(bw) : 0u;
+                    const uint32_t key = bw ? (p0 + ls + 1) << 16 | dls : 0u;
+                    const uint32_t inc = wave_incl_max_dpp(key);
+                    uint32_t cur = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)inc, 0x138, 0xf, 0xf, false); // wave_shr:1
+                    cur = (cur > carry ? cur : carry) & 0xffffu;
+                    carry = rl(inc, 63) > carry ? rl(inc, 63) : carry;
+#pragma unroll
+                    for (int i = 0; i < 16; i++) {
+                        cur = (bw >> i) & 1u ? (dv[i >> 1] >> (16 * (i & 1))) & 0xffffu : cur;
+                        const uint32_t p = p0 + i;
+                        sp[i] = p < lim && cur ? p - cur : p;
+                    }
+#else
                     const uint32_t cnt = (uint32_t)__builtin_popcount(bw);
                     const uint32_t incl = wave_incl_scan_dpp(cnt);
                     const uint32_t base = before + incl - cnt; // record starts before p0
                     before += rl(incl, 63);
-                    uint32_t sp[16];
 #pragma unroll
                     for (int i = 0; i < 16; i++) {
                         const uint32_t pr = base + (uint32_t)__builtin_popcount(bw & ((2u << i) - 1));
@@ -590,6 +637,8 @@ __global__ void __launch_bounds__(64) inflate_rec_kernel(InflateArgs a) {
                         const uint32_t p = p0 + i;
                         sp[i] = p < lim && sp[i] ? p - sp[i] : p;
                     }
+#endif
+                    // (a lane reads and then rewrites only its own 16 positions of src: no sync needed here)
                     uint32_t sw[8];
 #pragma unroll
                     for (int i = 0; i < 8; i++) sw[i] = sp[2 * i] | sp[2 * i + 1] << 16;
