@@ -364,8 +364,9 @@ PMC_API int pmc_ctx_create(int device, pmc_ctx **out) {
                                 (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)deflate_small_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kLdsPerCu));
-    HIP_TRY(hipFuncSetAttribute((const void *)deflate_front_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)kLdsPerCu));
+    for (const void *fk : {(const void *)deflate_front_kernel<0>, (const void *)deflate_front_kernel<1024>,
+                           (const void *)deflate_front_kernel<4096>})
+        HIP_TRY(hipFuncSetAttribute(fk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)deflate_back_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kLdsPerCu));
     HIP_TRY(hipFuncSetAttribute((const void *)deflate_trees_kernel<kTreesCap1K>,
@@ -782,8 +783,12 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
         const size_t tl_big = (size_t)(kLCodes + 1) * 64 * 4;
         // one pass over the batch for the values with lo < len <= hi, working sets sized for pcap
         auto run_pass = [&](uint64_t lo, uint64_t hi, uint64_t pcap) -> int {
-            const uint64_t fwb = deflate_front_wave_bytes(pcap), bwb = deflate_back_wave_bytes(pcap);
-            Launch Lf = plan_lds(ctx, (const void *)deflate_front_kernel, fwb, n, 0);
+            const uint32_t fcap = front_cap_class(pcap);
+            const uint64_t fwb = deflate_front_wave_bytes(fcap ? fcap : pcap), bwb = deflate_back_wave_bytes(pcap);
+            const void *fk = fcap == 1024   ? (const void *)deflate_front_kernel<1024>
+                             : fcap == 4096 ? (const void *)deflate_front_kernel<4096>
+                                            : (const void *)deflate_front_kernel<0>;
+            Launch Lf = plan_lds(ctx, fk, fwb, n, 0);
             const size_t front_lds = Lf.lds;
             Launch Lb = plan_lds(ctx, (const void *)deflate_back_kernel, bwb, n, kBackTabBytes);
             const uint64_t chunk = chunk_of(pcap), blocks = chunk / 64;
@@ -823,9 +828,13 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
                 a.wave_bytes = fwb;
                 if (hipMemsetAsync(a.cQ, 0, 8, st) != hipSuccess) return PMC_E_NO_DEVICE;
                 klaunch(ctx, PMC_K_DEFLATE_FRONT, st, [&] {
-                    hipLaunchKernelGGL(deflate_front_kernel,
-                                       dim3((unsigned)std::min<uint64_t>(Lf.blocks, (a.count + Lf.wpb - 1) / Lf.wpb)),
-                                       dim3(64 * Lf.wpb), front_lds, st, a);
+                    const dim3 fg((unsigned)std::min<uint64_t>(Lf.blocks, (a.count + Lf.wpb - 1) / Lf.wpb));
+                    if (fcap == 1024)
+                        hipLaunchKernelGGL(deflate_front_kernel<1024>, fg, dim3(64 * Lf.wpb), front_lds, st, a);
+                    else if (fcap == 4096)
+                        hipLaunchKernelGGL(deflate_front_kernel<4096>, fg, dim3(64 * Lf.wpb), front_lds, st, a);
+                    else
+                        hipLaunchKernelGGL(deflate_front_kernel<0>, fg, dim3(64 * Lf.wpb), front_lds, st, a);
                 });
                 if (hipMemsetAsync(a.cD + a.count, 0, 4, st) != hipSuccess) return PMC_E_NO_DEVICE;
                 // trees visit order by used literal/length symbols (PMC_TREES_ORDER=0: index order)

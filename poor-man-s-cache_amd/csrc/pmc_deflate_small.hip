@@ -2315,7 +2315,7 @@ struct SmallWave {
         PMC_STOP(21, 0)
         const uint32_t crc = wave_crc32_s8(bw, len, crc_tab); // (crc_tab: the back's slicing-by-8 tables)
         PMC_STOP(22, 0)
-        for (uint64_t k = l; k < out_words; k += 64) outw[k] = 0;
+        for (uint32_t k = l; k < out_words; k += 64) outw[k] = 0;
         wave_sync();
         if (l < 10) {
             const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 2, 3};
@@ -2329,7 +2329,7 @@ struct SmallWave {
         PMC_STOP(24, 0)
         PMC_STOP(25, 0)
         stamp(0); // (the back's times share slot 0: slots 3-5 count the front's eval usage)
-        uint64_t nbytes = bitpos >> 3;
+        uint32_t nbytes = (uint32_t)(bitpos >> 3); // (< 64 KiB: a small value's member)
         if (l < 8) {
             uint32_t v = l < 4 ? crc : len;
             outb[nbytes + l] = (uint8_t)(v >> (8 * (l & 3)));
@@ -2339,11 +2339,11 @@ struct SmallWave {
         if (nbytes > dst_cap) return PMC_E_CAPACITY_DEV;
         if ((((uintptr_t)dst) & 3) == 0) {
             uint32_t *d4 = reinterpret_cast<uint32_t *>(dst);
-            const uint64_t full = nbytes >> 2;
-            for (uint64_t k = l; k < full; k += 64) d4[k] = outw[k];
-            if ((uint64_t)l < (nbytes & 3)) dst[full * 4 + l] = outb[full * 4 + l];
+            const uint32_t full = nbytes >> 2;
+            for (uint32_t k = l; k < full; k += 64) d4[k] = outw[k];
+            if ((uint32_t)l < (nbytes & 3)) dst[full * 4 + l] = outb[full * 4 + l];
         } else {
-            for (uint64_t k = l; k < nbytes; k += 64) dst[k] = outb[k];
+            for (uint32_t k = l; k < nbytes; k += 64) dst[k] = outb[k];
         }
         if (l == 0) *dst_len = (uint32_t)nbytes;
         stamp(0);

@@ -29,12 +29,16 @@ namespace pmc {
 
 // ---- front -------------------------------------------------------------------------------------
 // (7 waves per SIMD: 72 VGPRs; 28 resident waves per CU at 1 KiB, which the LDS also allows)
+// CAPC != 0: the working set is laid out for CAPC bytes at compile time (front_cap_class), so the
+// kernel holds one parse instance and its LDS arrays sit at constant offsets from the wave's base.
+template <uint32_t CAPC>
 __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int wpb = blockDim.x / 64, wib = threadIdx.x / 64, l = lane_id();
-    uint8_t *base = lds + (uint64_t)wib * a.wave_bytes;
-    const SmallLayout L = small_layout(a.cap_len);
-    const FrontLayout F = front_layout(a.cap_len);
+    const uint64_t lcap = CAPC ? (uint64_t)CAPC : a.cap_len;
+    uint8_t *base = lds + (uint64_t)wib * (CAPC ? front_layout(lcap).total : a.wave_bytes);
+    const SmallLayout L = small_layout(lcap);
+    const FrontLayout F = front_layout(lcap);
     SmallWave w;
     small_wave_init(w, base, L, a, nullptr);
     w.S = to_lds<uint16_t>(base + F.S);
@@ -43,7 +47,7 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     w.HC = to_lds<uint64_t>(base + F.hc);
     w.EV = to_lds<uint32_t>(base + F.ev);
     w.cnp = F.pkb;
-    w.s12 = front_s12(a.cap_len) ? 1u : 0u;
+    w.s12 = front_s12(lcap) ? 1u : 0u;
     w.lfreq = to_lds<uint32_t>(base + F.freq);
     w.dfreq = w.lfreq + 288;
     w.blfreq = w.dfreq + 32;
@@ -94,6 +98,9 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
     }
     small_wave_stamps_out(w, a);
 }
+template __global__ void deflate_front_kernel<0>(DeflateArgs);
+template __global__ void deflate_front_kernel<1024>(DeflateArgs);
+template __global__ void deflate_front_kernel<4096>(DeflateArgs);
 
 // ---- trees (one lane per value) ------------------------------------------------------------------
 // (RegU16, pmc_device.hpp: round 5 moved bl_count and the bit-length frequencies from the lane's LDS column

@@ -192,7 +192,16 @@ uint64_t deflate_lv_emit_wave_bytes(uint64_t n);
 __global__ void deflate_small_kernel(DeflateArgs a);
 uint64_t deflate_front_wave_bytes(uint64_t n);
 uint64_t deflate_back_wave_bytes(uint64_t n);
+template <uint32_t CAPC>
 __global__ void deflate_front_kernel(DeflateArgs a);
+// the front instance for a pass of cap pcap: 1024 / 4096 (compile-time layout) or 0 (runtime layout)
+#ifndef PMC_FRONT_CAPC
+#define PMC_FRONT_CAPC 1
+#endif
+inline uint32_t front_cap_class(uint64_t pcap) {
+    if (!PMC_FRONT_CAPC) return 0u;
+    return pcap > 512 && pcap <= 1024 ? 1024u : pcap > 3072 && pcap <= 4096 ? 4096u : 0u;
+}
 template <int CAP>
 __global__ void deflate_trees_kernel(DeflateArgs a);
 __global__ void deflate_back_kernel(DeflateArgs a);
