@@ -62,7 +62,11 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
         if (g >= a.count) break;
         nx = l == 0 ? atomicAdd(a.cQ, kBatch) : 0u;
         const uint64_t vl = g + (uint64_t)l;
-        const uint32_t myl = (uint32_t)l < kBatch && vl < a.count ? a.src_len[a.first + vl] : 0u;
+        const bool in = (uint32_t)l < kBatch && vl < a.count;
+        const uint32_t myl = in ? a.src_len[a.first + vl] : 0u;
+        // (source offsets load with the lengths: no dependent round trip per value for its address.  An L2
+        // prefetch of the grab's next value beside this one's stage loads measured no faster: round 6)
+        const uint64_t myo = in ? a.src_off[a.first + vl] : 0u;
         uint64_t todo = ballot(myl != 0 && myl > a.min_len && myl <= a.lds_max_len);
         while (todo) {
             const int jj = __builtin_ctzll(todo);
@@ -73,7 +77,8 @@ __global__ void __launch_bounds__(256, 7) deflate_front_kernel(DeflateArgs a) {
 #ifdef PMC_FAULT_LANE_ORDER // (odd values fail the sort's guard; the even ones reach the back's code-rank guard)
             w.fault_rev = (uint32_t)(gv & 1);
 #endif
-            const uint32_t ntok = w.run_front(a.src + a.src_off[gv], len);
+            const uint8_t *vsrc = a.src + readlane64(myo, jj);
+            const uint32_t ntok = w.run_front(vsrc, len);
             if (ntok == kNtokRetry) { // the sort's lane-order guard fired: the HBM kernel redoes the value
                 if (l == 0) {
                     a.cN[v] = kNtokRetry;
