@@ -313,6 +313,19 @@ constexpr uint32_t kPreCandLanes = 32;
 #ifndef PMC_EVAL_CN1DPP
 #define PMC_EVAL_CN1DPP 1
 #endif
+// PMC_EVAL_PRED (values <= 1 KiB, PK 6): build_cn stores each position's match length with its nearest
+// candidate (capped at 32) in the spare top bits of its S entry; an eval runs deflate_slow's lazy walk over
+// those lengths for up to kPredHops fresh starts and gives lanes only to the positions that walk visits,
+// instead of to every position of the window in order (a round-6 simulation of 1 KiB JSON slices: 38.8 ->
+// 24.7 evals per value; the stamps build measured 37.5 -> 23.8).  The walk itself stays exact: a needed position the prediction left out is a
+// stop, and the next eval starts there.
+#ifndef PMC_EVAL_PRED
+#define PMC_EVAL_PRED 1
+#endif
+// (same box, 10M x 1 KiB: front 175.3 -> 173.5 ms at 3 hops, 173.9 at 4; lengths capped at 16 instead of
+// 32: 177.4 -- more misses; the hops as a scalar loop over the masks instead of per-lane precomputed
+// targets: 196 ms, the scalar unit saturated)
+constexpr uint32_t kPredHops = 3, kPredCap = 32;
 // (the fault build runs the u32-counter sort's first scatter from the loop below, whose lanes it reverses)
 #ifdef PMC_FAULT_LANE_ORDER
 #define PMC_FAULT_PASS0 0
@@ -388,6 +401,8 @@ struct SmallWave {
             PMC_LDS const uint32_t *S32 = (PMC_LDS const uint32_t *)S;
             const uint32_t bit = 12u * k, w = bit >> 5;
             return __builtin_amdgcn_alignbit(S32[w + 1], S32[w], bit & 31u) & 0xfffu;
+        } else if constexpr (PK == 6 && PMC_EVAL_PRED) {
+            return S[k] & 0x3ffu; // (bits 15:10: the nearest candidate's match length, PMC_EVAL_PRED)
         } else {
             return S[k];
         }
@@ -933,7 +948,7 @@ struct SmallWave {
         }
     }
     template <int PK>
-    __device__ __forceinline__ uint32_t build_cn(uint32_t npos, uint32_t k0) {
+    __device__ __forceinline__ uint32_t build_cn(uint32_t npos, uint32_t k0, uint32_t len_) {
         constexpr uint32_t RB = 16 - (PK > 0 ? PK : 0), CMAX = PK > 0 ? (1u << PK) - 1 : 255u;
         const uint32_t l = (uint32_t)lane_id();
         // has-candidate bits set by position below (HC as u32 words, LDS atomics): no second
@@ -945,14 +960,46 @@ struct SmallWave {
         }
         uint32_t ph = 0xffffffffu, prs = 0, pq = 0; // previous chunk's last hash, run start, position
         uint32_t bad = 0;
+        constexpr bool kPred = PK == 6 && PMC_EVAL_PRED;
+        uint32_t pa[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // (kPred) previous chunk's last 32 bytes
         for (uint32_t c0 = 0; c0 < npos; c0 += 64) {
             const uint32_t k = c0 + l;
             const bool valid = k < npos;
             const uint32_t p = valid ? sget<PK>(k) : 0u;
-            const uint32_t h = valid ? hash3(load4(p)) : 0xfffffffeu;
+            uint32_t h;
+            uint32_t a[8];
+            if constexpr (kPred) { // 32 bytes at p; the nearest candidate's are lane l - 1's
+                uint64_t A0, A1, A2 = 0, A3 = 0;
+                load16(p, A0, A1);
+                if (kPredCap > 16) load16(p + 16, A2, A3);
+                a[0] = (uint32_t)A0, a[1] = (uint32_t)(A0 >> 32), a[2] = (uint32_t)A1, a[3] = (uint32_t)(A1 >> 32);
+                a[4] = (uint32_t)A2, a[5] = (uint32_t)(A2 >> 32), a[6] = (uint32_t)A3, a[7] = (uint32_t)(A3 >> 32);
+                h = valid ? hash3(a[0]) : 0xfffffffeu;
+            } else {
+                h = valid ? hash3(load4(p)) : 0xfffffffeu;
+            }
             uint32_t hp = (uint32_t)__shfl_up((int)h, 1), pp = (uint32_t)__shfl_up((int)p, 1);
             hp = l == 0 ? ph : hp;
             pp = l == 0 ? pq : pp;
+            if constexpr (kPred) {
+                // match length with pp (same hash, not NIL), capped at 32 and at the bytes left
+                uint32_t x8[8];
+                constexpr int kW = kPredCap / 4;
+#pragma unroll
+                for (int i = 0; i < kW; i++) {
+                    const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp((int)pa[i], (int)a[i], 0x138, 0xf, 0xf, false);
+                    x8[i] = a[i] ^ b; // (wave_shr:1: lane 0 keeps the previous chunk's lane 63)
+                    pa[i] = readlane(a[i], 63);
+                }
+                // leading equal bytes: the first differing dword's lowest set byte (kW * 4 when none)
+                uint32_t m = 4u * kW;
+#pragma unroll
+                for (int i = kW - 1; i >= 0; i--) m = x8[i] ? 4u * i + ((uint32_t)__builtin_ctz(x8[i]) >> 3) : m;
+                const uint32_t left = len_ - p;
+                m = m < left ? m : left;
+                m = valid && k != 0 && h == hp && pp != 0u ? m : 0u;
+                if (valid) S[k] = (uint16_t)(p | m << 10);
+            }
             // (hash, position) must increase: h > hp, or h == hp and p > pp (k = 0 has no predecessor)
             bad |= (valid && k != 0 && (h < hp || (h == hp && p <= pp))) ? 1u : 0u;
             uint32_t rs = wave_incl_max_dpp(valid && h != hp ? k : 0u);
@@ -1005,7 +1052,8 @@ struct SmallWave {
     // (5) an LDS max per position and its read-back.  Lanes outside the evaluated prefix
     // compute on clamped indices and contribute key 0 (no exec-mask branches).
     template <int PK>
-    __device__ void eval_group(Group &g, uint32_t p0, uint32_t npos, uint32_t len) {
+    // (pend: the walk's pending match length at p0, 2 = none; it seeds PMC_EVAL_PRED's predicted walk)
+    __device__ void eval_group(Group &g, uint32_t p0, uint32_t npos, uint32_t len, uint32_t pend = 2) {
         // SAT: a count field narrower than kPreCand saturates below it; such a position gets
         // kPreCand lanes whose candidates are validated (same hash, inside the array, not NIL) and
         // is marked cut (search() resumes it exactly if the parse needs it)
@@ -1035,7 +1083,44 @@ struct SmallWave {
         else cn1 = CN[x1];
         cn1 = x + 1 < npos ? cn1 : 0u;
 #endif
-        const uint32_t w0 = SAT && cn == CMAX ? kPreCand : cn < kPreCand ? cn : kPreCand;
+        uint32_t gate = 1; // (PMC_EVAL_PRED: 0 for a position the predicted walk skips)
+#if PMC_EVAL_PRED
+        if constexpr (PK == 6) {
+            // deflate_slow's lazy walk from p0 over the nearest candidates' match lengths (S bits 15:10):
+            // from a fresh start s it visits s .. t, t the first position after s that does not improve
+            // on its predecessor's length, and starts afresh at t - 1 + that length
+            const uint32_t l1 = (uint32_t)S[rx] >> 10;
+            const uint32_t ml = cn != 0u && l1 >= 3u ? l1 : 2u;
+            const uint32_t mlp = (uint32_t)__builtin_amdgcn_update_dpp((int)pend, (int)ml, 0x138, 0xf, 0xf, false); // lane l - 1's; lane 0: pend
+            const uint64_t hcm = ballot(cn != 0u), impm = ballot(ml > mlp);
+            // per lane l, as a fresh start: T = the first later offset that does not improve (64: none), the
+            // offsets it visits (rm: l .. T, or l alone without a match) and the next fresh start with
+            // candidates (jn); the hops then cost two-three readlanes each on the scalar side
+            const uint32_t lp1 = l + 1u;
+            const uint64_t nim = lp1 < 64u ? ~impm & (~0ull << lp1) : 0ull;
+            const uint32_t T = nim ? (uint32_t)__builtin_ctzll(nim) : 64u;
+            const uint32_t mlt = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((T - 1u) & 63u) << 2), (int)ml);
+            const uint32_t J = ml < 3u ? lp1 : T - 1u + mlt;
+            const uint64_t hj = J < 64u ? hcm & (~0ull << J) : 0ull;
+            const uint32_t jn = hj ? (uint32_t)__builtin_ctzll(hj) : 64u;
+            const uint64_t rm = ml < 3u ? 1ull << l : (T >= 63u ? ~0ull : (2ull << T) - 1ull) & (~0ull << l);
+            uint64_t inc = 1; // (offset 0: the position the walk asks for)
+            uint32_t sp = 0;
+            if (pend >= 3 && !(impm & 1)) { // a pending match that p0 does not improve on: next start p0 + pend - 1
+                const uint64_t m = pend - 1u < 64u ? hcm & (~0ull << (pend - 1u)) : 0ull;
+                sp = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+            }
+#pragma unroll
+            for (uint32_t h = 0; h < kPredHops; h++) {
+                if (sp >= 64u) break;
+                inc |= readlane64(rm, (int)sp);
+                sp = readlane(jn, (int)sp);
+            }
+            if (sp < 64u) inc |= ~0ull << sp; // (past the hop limit: the rest of the window in order)
+            gate = (uint32_t)(inc >> l) & 1u;
+        }
+#endif
+        const uint32_t w0 = gate == 0u ? 0u : SAT && cn == CMAX ? kPreCand : cn < kPreCand ? cn : kPreCand;
         const uint32_t w = w0; // lanes of this position
         const uint32_t incl = wave_incl_scan_dpp(w), offs = incl - w;
         const bool inc = w != 0 && incl <= 64;
@@ -1224,11 +1309,11 @@ struct SmallWave {
     }
     // longest_match record of has-candidate position x (evaluating a new window if needed)
     template <int PK>
-    __device__ uint32_t group_get(Group &g, uint32_t x, uint32_t npos, uint32_t len) {
+    __device__ uint32_t group_get(Group &g, uint32_t x, uint32_t npos, uint32_t len, uint32_t pend) {
         const uint32_t off = x - g.p0;
         if (off < 64 && ((g.m >> off) & 1)) return readlane(g.e, (int)off);
         stamp(2);
-        eval_group<PK>(g, x, npos, len);
+        eval_group<PK>(g, x, npos, len, pend);
         stamp(10);
         count(13);
         return readlane(g.e, 0);
@@ -1250,7 +1335,7 @@ struct SmallWave {
     __device__ __forceinline__ uint32_t parse_ondemand_body(uint32_t npos_, uint32_t len_, uint32_t k0_) {
         const uint32_t npos = rfl(npos_), len = rfl(len_); // (arguments arrive in VGPRs)
         const uint32_t nw = (npos + 63) >> 6;
-        if (sflag(build_cn<PK>(npos, rfl(k0_)))) return kNtokRetry; // (the sort's lane-order guard)
+        if (sflag(build_cn<PK>(npos, rfl(k0_), len))) return kNtokRetry; // (the sort's lane-order guard)
         stamp(11);
         PMC_STOP(13, 0)
         Group g;
@@ -1368,7 +1453,7 @@ struct SmallWave {
                     if (!(i - g.p0 < 64 && ((g.m >> (i - g.p0)) & 1))) PMC_D_EVAL(i);
                     PMC_D_USE(i - g.p0, i - g.p0);
 #endif
-                    const uint32_t e = group_get<PK>(g, i, npos, len);
+                    const uint32_t e = group_get<PK>(g, i, npos, len, pl);
                     uint32_t m = e & 511, q = (e >> 9) & 0x7fffu;
                     if (e >> 31) {
                         stamp(2);
