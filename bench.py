@@ -602,7 +602,10 @@ def main():
                     tj = json.load(f)
                 if (tj.get("n") == n and tj.get("vlen") == vlen and tj.get("kind") == args.kind
                         and tj.get("source_id") == pmc_codec.source_id()):
-                    kj = tj.get("kernels", {}).get(pmc_codec.KERNEL_NAMES[dom], {})
+                    # (a templated kernel is listed per instance, "name<1024u>": the one this workload ran)
+                    kn, ks = pmc_codec.KERNEL_NAMES[dom], tj.get("kernels", {})
+                    inst = [k for k in ks if k == kn or k.startswith(kn + "<")]
+                    kj = max((ks[k] for k in inst), key=lambda e: e.get("launches", 0), default={})
                     traffic = kj.get("hbm_bytes_per_launch")
                     issue = kj.get("issue")
                     tsrc = os.path.relpath(args.traffic, ROOT)
