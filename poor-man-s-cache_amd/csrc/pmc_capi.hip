@@ -765,6 +765,7 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
         auto scratch_of = [&](uint64_t c, uint64_t ch) {
             const uint64_t blocks = ch / 64;
             return ch * c * 4 + ch * 4 + ch * 4 + blocks * 64 * kSplitRows * 3 + blocks * 64 * kMergeRows * 4 +
+                   blocks * 64 * kHdrWords * 4 +
                    (ch + 1) * 4 + ch * 8 + kOrderBins * 4 + 64 + 1024;
         };
         uint64_t need = scratch_of(cap, chunk_of(cap));
@@ -805,6 +806,8 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
             p += blocks * 64 * kSplitRows * 2;
             a.cL = (uint8_t *)p;
             p += blocks * 64 * kSplitRows;
+            a.cB = (uint32_t *)p;
+            p += blocks * 64 * kHdrWords * 4;
             a.cD = (uint32_t *)p;
             p += (chunk + 1) * 4;
             a.cZ = (uint32_t *)p;

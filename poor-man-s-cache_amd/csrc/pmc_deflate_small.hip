@@ -364,6 +364,7 @@ struct SmallWave {
     PMC_LDS uint64_t *ML;   // segment walk: positions that start a match (or are unresolved)
     PMC_LDS uint64_t *MP;   // segment walk: positions where a lazy-improvement run ends
     PMC_GLB uint32_t *tok;
+    PMC_GLB const uint32_t *hdr = nullptr; // split back: this value's tree header from the trees kernel
     Trees *fb; // HBM scratch for the serial fallback
     PMC_LDS const uint32_t *crc_tab;
     PMC_LDS uint16_t *perm; // split back: the code-rank guard's canonical order (BackLayout::perm)
@@ -2283,6 +2284,31 @@ struct SmallWave {
             // (lcode | dcode | blcode contiguous; runs is free scratch in the split back)
             if (sflag(codes_from_lengths_all(Ls, lcode, (PMC_LDS uint32_t *)runs, perm))) return kBitsGuard;
             PMC_STOP(23, bitpos)
+#if PMC_TREES_HDR
+            if (sflag(hdr ? 1u : 0u)) { // the header bits the trees kernel emitted, after the 3-bit block header
+                if (l == 0) or_bits_lds(bitpos, (2u << 1) | 1u, 3);
+                bitpos += 3;
+                const uint32_t hb = rfl(hdr[0]), nw = (hb + 31) / 32, sh = (uint32_t)(bitpos & 31);
+                const uint64_t w0 = bitpos >> 5;
+                wave_sync();
+                for (uint32_t k = (uint32_t)l; k < nw; k += 64) {
+                    const uint32_t x = hdr[1 + k];
+                    lds_or(&outw[w0 + k], x << sh);
+                    if (sh && (x >> (32 - sh))) lds_or(&outw[w0 + k + 1], x >> (32 - sh));
+                }
+                bitpos += hb;
+                wave_sync();
+                PMC_STOP(24, bitpos)
+                bitpos = emit_symbols(ntok, bitpos);
+                const uint32_t eob = lcode[kEndBlock];
+                wave_sync();
+                if (l == 0) or_bits_lds(bitpos, eob & 0xffff, (int)(eob >> 16));
+                bitpos += eob >> 16;
+                bitpos = (bitpos + 7) & ~(uint64_t)7;
+                wave_sync();
+                return bitpos;
+            }
+#endif
             const int lcodes = l_max + 1, dcodes = d_max + 1, blcodes = mbi + 1;
             if (l == 0) {
                 or_bits_lds(bitpos, (2u << 1) | 1u, 3);

@@ -327,6 +327,104 @@ struct LaneTrees {
         return max_code;
     }
 
+    // send_all_trees (trees.c) of a dynamic block, per lane: HLIT, HDIST, HCLEN, the bit-length code lengths
+    // in bl_order, then send_tree over the staged lit/len and distance lengths; the bits go LSB-first to
+    // row[1..], their count to row[0].  (The back, a wave per value, spent a third of its time on these
+    // serial runs; here one instruction serves 64 values.)  blw: row bytes 304..335 (bl lengths at 12..30).
+    __device__ void emit_header(int l_max, int d_max, int mbi, const uint32_t *blw, PMC_GLB uint32_t *row) {
+        auto blen = [&](int s) -> uint32_t { return (blw[(12 + s) >> 2] >> (8 * ((12 + s) & 3))) & 0xffu; };
+        // canonical bit-length codes (gen_codes): counts and next codes as bytes of 64-bit words
+        uint64_t cnt = 0;
+#pragma unroll
+        for (int s = 0; s < kBLCodes; s++) {
+            const uint32_t L = blen(s);
+            cnt += L ? 1ull << (8 * L) : 0ull;
+        }
+        uint64_t nc = 0;
+        uint32_t code = 0;
+#pragma unroll
+        for (int b = 1; b <= kMaxBLBits; b++) {
+            code = (code + (uint32_t)((cnt >> (8 * (b - 1))) & 0xffu)) << 1;
+            nc |= (uint64_t)code << (8 * b);
+        }
+        RegU16<kBLCodes> bc; // code | len << 8 per bit-length symbol
+#pragma unroll
+        for (int s = 0; s < kBLCodes; s++) {
+            const uint32_t L = blen(s), c = (uint32_t)(nc >> (8 * L)) & 0xffu;
+            nc += L ? 1ull << (8 * L) : 0ull;
+            bc.set((uint32_t)s, L ? (__builtin_bitreverse32(c) >> (32 - L)) | L << 8 : 0u);
+        }
+        uint64_t acc = 0;
+        uint32_t an = 0, wi = 1, total = 0;
+        auto put = [&](uint32_t v, uint32_t n) {
+            acc |= (uint64_t)v << an;
+            an += n;
+            total += n;
+            if (an >= 32) {
+                row[wi++] = (uint32_t)acc;
+                acc >>= 32;
+                an -= 32;
+            }
+        };
+        auto send_code = [&](uint32_t sym) {
+            const uint32_t e = bc.get(sym);
+            put(e & 0xffu, e >> 8);
+        };
+        put((uint32_t)(l_max + 1 - 257), 5);
+        put((uint32_t)d_max, 5);
+        put((uint32_t)(mbi + 1 - 4), 4);
+        for (int k = 0; k <= mbi; k++) put(bc.get(bl_order_cf(k)) >> 8, 3);
+        for (int tr = 0; tr < 2; tr++) { // send_tree: the lit/len tree, then the distance tree
+            const uint32_t row0 = tr ? (uint32_t)kLCodes : 0u;
+            const int max_code = tr ? d_max : l_max;
+            int prevlen = -1, nextlen = (int)lrow(row0), count = 0, max_count = 7, min_count = 4;
+            if (nextlen == 0) max_count = 138, min_count = 3;
+            int w0 = -8;
+            uint64_t pk = 0;
+            for (int n = 0; n <= max_code; n++) {
+                const int curlen = nextlen, nx = n + 1;
+                if (nx <= max_code) {
+                    if (nx >= w0 + 8) {
+                        w0 = nx & ~7;
+                        pk = 0;
+#pragma unroll
+                        for (int k = 0; k < 8; k++)
+                            pk |= (uint64_t)(w0 + k <= max_code ? lrow(row0 + (uint32_t)(w0 + k)) : 0u) << (8 * k);
+                    }
+                    nextlen = (int)((pk >> (8 * (nx - w0))) & 0xff);
+                } else {
+                    nextlen = 0xffff;
+                }
+                if (++count < max_count && curlen == nextlen) continue;
+                if (count < min_count) {
+                    do {
+                        send_code((uint32_t)curlen);
+                    } while (--count != 0);
+                } else if (curlen != 0) {
+                    if (curlen != prevlen) {
+                        send_code((uint32_t)curlen);
+                        count--;
+                    }
+                    send_code(kRep3_6);
+                    put((uint32_t)(count - 3), 2);
+                } else if (count <= 10) {
+                    send_code(kRepz3_10);
+                    put((uint32_t)(count - 3), 3);
+                } else {
+                    send_code(kRepz11_138);
+                    put((uint32_t)(count - 11), 7);
+                }
+                count = 0;
+                prevlen = curlen;
+                if (nextlen == 0) max_count = 138, min_count = 3;
+                else if (curlen == nextlen) max_count = 6, min_count = 3;
+                else max_count = 7, min_count = 4;
+            }
+        }
+        if (an) row[wi] = (uint32_t)acc;
+        row[0] = total;
+    }
+
     // byte j of the lengths row as staged in the heap column (stage_row)
     __device__ uint32_t lrow(uint32_t j) const { return (hp[(j >> 2) * 64] >> (8 * (j & 3))) & 0xffu; }
     // The lit/len + distance lengths (row bytes 0..319) into the heap column, free between the distance
@@ -447,7 +545,12 @@ __device__ void trees_value(const DeflateArgs &a, uint64_t v, uint64_t slot, PMC
     const uint32_t static_lenb = (stat + 3 + 7) >> 3;
     if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
     const uint32_t type = len + 4 <= opt_lenb ? 0u : static_lenb == opt_lenb ? 1u : 2u;
-    a.cP[v] = type | (uint32_t)l_max << 2 | (uint32_t)d_max << 11 | (uint32_t)mbi << 16;
+    const bool hdr = PMC_TREES_HDR && type == 2 && len > kHdrMinLen;
+    a.cP[v] = type | (uint32_t)l_max << 2 | (uint32_t)d_max << 11 | (uint32_t)mbi << 16 | (hdr ? kPlanHdr : 0u);
+    if (hdr) { // (the bit-length tree's heap overwrote the front of the staged row: stage it again)
+        t.stage_row();
+        t.emit_header(l_max, d_max, mbi, blw, (PMC_GLB uint32_t *)(a.cB + v * kHdrWords));
+    }
 }
 
 // Values whose literal/length tree needs more than CAP heap entries are listed in cD (count at
@@ -562,6 +665,7 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
                 for (uint32_t k = l; k < kSplitRows / 4; k += 64) Lw[k] = row[k];
             }
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
+            w.hdr = plan & kPlanHdr ? (PMC_GLB const uint32_t *)(a.cB + v * kHdrWords) : nullptr;
             const int rc = w.run_back(a.src + readlane64(myo, j), len, ntok, plan, Ls, a.dst + readlane64(mydo, j),
                                       readlane(myc, j), a.dst_len + gv);
             if (l == 0) {

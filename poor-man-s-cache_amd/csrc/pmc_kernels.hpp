@@ -45,6 +45,7 @@ struct DeflateArgs {
     uint32_t *cN;  // token count per value
     uint16_t *cH;  // symbol histograms, [value][kSplitRows]
     uint8_t *cL;   // code lengths lit/len | dist | bit-length, [value][kSplitRows]
+    uint32_t *cB;  // dynamic-block tree headers from the trees kernel, [value][kHdrWords] (PMC_TREES_HDR)
     uint32_t *cP;  // block plan per value
     uint32_t *cG;  // trees kernel merge lists, interleaved [block][kMergeRows][64]
     uint32_t *cD;  // values deferred to the large-heap trees pass; their number at cD[count]
@@ -118,6 +119,17 @@ constexpr uint32_t kNtokRetry = 0xfffffffeu;      // cN marker: the sort's lane-
 constexpr uint32_t kBackTabBytes = 8 * 256 * 4; // the back kernel's slicing-by-8 CRC tables (LDS per block)
 constexpr uint32_t kSplitRows = 336;  // 286 lit/len + 30 dist + 19 bit-length (+1)
 constexpr uint32_t kMergeRows = 572;  // 2 heap entries per merge, <= 285 merges
+// a dynamic block's tree header (HLIT..send_tree, at most 14 + 19 * 3 + 316 * 7 = 2283 bits): word 0 the
+// bit count, then the bits LSB-first (76 words: 16-byte rows)
+constexpr uint32_t kHdrWords = 76;
+// PMC_TREES_HDR: for values of more than kHdrMinLen bytes the trees kernel (one lane per value) emits the
+// header bits and sets kPlanHdr in the plan; the back copies them.  (Same box, 10M x 1 KiB: trees 20.6 ->
+// 27.8 ms, back 36.7 -> 26.3; 1M x 4 KiB: -1.2 ms; at 256 B the trees' cost exceeded the back's saving,
+// +6.8 / -5.4 ms, so smaller values keep the back's wave-wide headers.)
+#ifndef PMC_TREES_HDR
+#define PMC_TREES_HDR 1
+#endif
+constexpr uint32_t kHdrMinLen = 512, kPlanHdr = 1u << 21;
 constexpr uint32_t kPlanDeferred = 0xffffffffu;
 #ifndef PMC_TREES_CAP
 #define PMC_TREES_CAP 84
