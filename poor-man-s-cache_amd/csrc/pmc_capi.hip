@@ -765,7 +765,7 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
         auto scratch_of = [&](uint64_t c, uint64_t ch) {
             const uint64_t blocks = ch / 64;
             return ch * c * 4 + ch * 4 + ch * 4 + blocks * 64 * kSplitRows * 3 + blocks * 64 * kMergeRows * 4 +
-                   blocks * 64 * kHdrWords * 4 +
+                   blocks * 64 * kHdrWords * 4 + ch * 4 +
                    (ch + 1) * 4 + ch * 8 + kOrderBins * 4 + 64 + 1024;
         };
         uint64_t need = scratch_of(cap, chunk_of(cap));
@@ -808,6 +808,8 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
             p += blocks * 64 * kSplitRows;
             a.cB = (uint32_t *)p;
             p += blocks * 64 * kHdrWords * 4;
+            a.cC = (uint32_t *)p;
+            p += chunk * 4;
             a.cD = (uint32_t *)p;
             p += (chunk + 1) * 4;
             a.cZ = (uint32_t *)p;
@@ -862,6 +864,14 @@ static int compress_batch_body(pmc_ctx *ctx, const uint8_t *src, const uint64_t 
                                        dim3(64), tl_big, st, a);
                 });
                 a.wave_bytes = bwb;
+                a.back_nostage = PMC_BACK_NOSTAGE && pcap <= kNostageMaxLen ? 1u : 0u;
+                // the values' CRC-32 for the back (counted with the back: it is the back's work moved out)
+                if (a.back_nostage) klaunch(ctx, PMC_K_DEFLATE_BACK, st, [&] {
+                    const unsigned cb = (unsigned)std::min<uint64_t>((a.count + 511) / 512, (uint64_t)ctx->cus * 4);
+                    hipLaunchKernelGGL(crc32_batch_kernel, dim3(cb), dim3(512), 0, st, (const uint8_t *)a.src,
+                                       (const uint64_t *)(a.src_off + a.first), (const uint32_t *)(a.src_len + a.first),
+                                       a.count, a.cC);
+                });
                 klaunch(ctx, PMC_K_DEFLATE_BACK, st, [&] {
                     hipLaunchKernelGGL(deflate_back_kernel,
                                        dim3((unsigned)std::min<uint64_t>(Lb.blocks, (a.count + Lb.wpb - 1) / Lb.wpb)),

@@ -365,6 +365,7 @@ struct SmallWave {
     PMC_LDS uint64_t *MP;   // segment walk: positions where a lazy-improvement run ends
     PMC_GLB uint32_t *tok;
     PMC_GLB const uint32_t *hdr = nullptr; // split back: this value's tree header from the trees kernel
+    PMC_GLB const uint8_t *gsrc = nullptr; // split back (PMC_BACK_NOSTAGE): the source bytes in HBM, not staged
     Trees *fb; // HBM scratch for the serial fallback
     PMC_LDS const uint32_t *crc_tab;
     PMC_LDS uint16_t *perm; // split back: the code-rank guard's canonical order (BackLayout::perm)
@@ -1863,6 +1864,7 @@ struct SmallWave {
     }
 
     // compress_block: every token's bits at its prefix-sum offset
+    template <bool G = false> // G: a literal's byte from gsrc (HBM) instead of the staged b
     __device__ uint64_t emit_symbols(uint32_t ntok, uint64_t bitpos) {
         const int l = lane_id();
         const Tables &TT = c_tables;
@@ -1871,7 +1873,8 @@ struct SmallWave {
             uint32_t nb = 0;
             uint64_t v = 0;
             if (t < ntok) {
-                const uint32_t tk = tok[t], dist = tk >> 16, lc = dist ? tk & 0xff : b[tk & 0xffff];
+                const uint32_t tk = tok[t], dist = tk >> 16;
+                const uint32_t lc = dist ? tk & 0xff : G ? (uint32_t)gsrc[tk & 0xffff] : (uint32_t)b[tk & 0xffff];
                 if (dist == 0) {
                     const uint32_t c = lcode[lc];
                     v = c & 0xffff;
@@ -2267,7 +2270,7 @@ struct SmallWave {
                 uint32_t v = l < 2 ? len : ~len;
                 outb[o + l] = (uint8_t)(v >> (8 * (l & 1)));
             }
-            for (uint32_t k = l; k < len; k += 64) outb[o + 4 + k] = b[k];
+            for (uint32_t k = l; k < len; k += 64) outb[o + 4 + k] = gsrc ? gsrc[k] : b[k];
             bitpos += (4 + (uint64_t)len) * 8;
             wave_sync();
             return bitpos;
@@ -2299,7 +2302,7 @@ struct SmallWave {
                 bitpos += hb;
                 wave_sync();
                 PMC_STOP(24, bitpos)
-                bitpos = emit_symbols(ntok, bitpos);
+                bitpos = sflag(gsrc ? 1u : 0u) ? emit_symbols<true>(ntok, bitpos) : emit_symbols<false>(ntok, bitpos);
                 const uint32_t eob = lcode[kEndBlock];
                 wave_sync();
                 if (l == 0) or_bits_lds(bitpos, eob & 0xffff, (int)(eob >> 16));
@@ -2326,7 +2329,7 @@ struct SmallWave {
             wave_sync();
             PMC_STOP(24, bitpos)
         }
-        bitpos = emit_symbols(ntok, bitpos);
+        bitpos = sflag(gsrc ? 1u : 0u) ? emit_symbols<true>(ntok, bitpos) : emit_symbols<false>(ntok, bitpos);
         const uint32_t eob = lcode[kEndBlock];
         wave_sync();
         if (l == 0) or_bits_lds(bitpos, eob & 0xffff, (int)(eob >> 16));
@@ -2420,11 +2423,19 @@ struct SmallWave {
     }
     // ---- split pipeline: back half (CRC, codes from the planned lengths, emission) -------
     __device__ int run_back(const uint8_t *src, uint32_t len, uint32_t ntok, uint32_t plan, PMC_LDS const uint8_t *Ls,
-                            uint8_t *dst, uint32_t dst_cap, uint32_t *dst_len) {
+                            uint8_t *dst, uint32_t dst_cap, uint32_t *dst_len, uint32_t crc_in, uint32_t nostage) {
         const int l = lane_id();
-        stage(src, len);
-        PMC_STOP(21, 0)
-        const uint32_t crc = wave_crc32_s8(bw, len, crc_tab); // (crc_tab: the back's slicing-by-8 tables)
+        uint32_t crc;
+        if (sflag(nostage)) { // (PMC_BACK_NOSTAGE: crc_in is the batch CRC pass's)
+            gsrc = (PMC_GLB const uint8_t *)src;
+            crc = crc_in;
+            PMC_STOP(21, 0)
+        } else {
+            gsrc = nullptr;
+            stage(src, len);
+            PMC_STOP(21, 0)
+            crc = wave_crc32_s8(bw, len, crc_tab); // (crc_tab: the back's slicing-by-8 tables)
+        }
         PMC_STOP(22, 0)
         for (uint32_t k = l; k < out_words; k += 64) outw[k] = 0;
         wave_sync();

@@ -612,6 +612,7 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
         const bool in = (uint32_t)l < kBatch && vl < a.count;
         const uint32_t myl = in ? a.src_len[a.first + vl] : 0u;
         const uint32_t myn = in ? a.cN[vl] : 0u, myp = in ? a.cP[vl] : 0u;
+        const uint32_t myk = a.back_nostage && in ? a.cC[vl] : 0u; // (the batch CRC pass's)
         // (source / destination offsets and capacities of the batch load with its lengths: no
         // dependent round trip per value for its addresses)
         const uint64_t myo = in ? a.src_off[a.first + vl] : 0u, mydo = in ? a.dst_off[a.first + vl] : 0u;
@@ -667,7 +668,7 @@ __global__ void __launch_bounds__(256, 5) deflate_back_kernel(DeflateArgs a) {
             w.tok = (PMC_GLB uint32_t *)(a.cT + v * a.cap_len);
             w.hdr = plan & kPlanHdr ? (PMC_GLB const uint32_t *)(a.cB + v * kHdrWords) : nullptr;
             const int rc = w.run_back(a.src + readlane64(myo, j), len, ntok, plan, Ls, a.dst + readlane64(mydo, j),
-                                      readlane(myc, j), a.dst_len + gv);
+                                      readlane(myc, j), a.dst_len + gv, readlane(myk, j), a.back_nostage);
             if (l == 0) {
                 a.rc[gv] = rc;
                 if (rc) a.dst_len[gv] = 0;

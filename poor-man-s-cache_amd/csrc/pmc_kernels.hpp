@@ -46,6 +46,8 @@ struct DeflateArgs {
     uint16_t *cH;  // symbol histograms, [value][kSplitRows]
     uint8_t *cL;   // code lengths lit/len | dist | bit-length, [value][kSplitRows]
     uint32_t *cB;  // dynamic-block tree headers from the trees kernel, [value][kHdrWords] (PMC_TREES_HDR)
+    uint32_t *cC;  // CRC-32 of each value of the chunk, from crc32_batch_kernel (PMC_BACK_NOSTAGE)
+    uint32_t back_nostage; // this pass's back reads cC and the source in HBM instead of staging (PMC_BACK_NOSTAGE)
     uint32_t *cP;  // block plan per value
     uint32_t *cG;  // trees kernel merge lists, interleaved [block][kMergeRows][64]
     uint32_t *cD;  // values deferred to the large-heap trees pass; their number at cD[count]
@@ -130,6 +132,15 @@ constexpr uint32_t kHdrWords = 76;
 #define PMC_TREES_HDR 1
 #endif
 constexpr uint32_t kHdrMinLen = 512, kPlanHdr = 1u << 21;
+// PMC_BACK_NOSTAGE: for passes of values of <= kNostageMaxLen bytes the back stages no source bytes: their
+// CRC-32 comes from a batch CRC pass before it (the verify kernel's method) and a literal token's byte is
+// read from the source in HBM (L2: the back's prefetch has touched its lines).  Same box: 10M x 256 B back
+// 23.35 -> 21.5 ms (CRC pass included); at 1 KiB 26.3 -> 27.65 and 4 KiB 11.4 -> 14.15, so larger values
+// keep the staged bytes and the back's own CRC.
+#ifndef PMC_BACK_NOSTAGE
+#define PMC_BACK_NOSTAGE 1
+#endif
+constexpr uint32_t kNostageMaxLen = 512;
 constexpr uint32_t kPlanDeferred = 0xffffffffu;
 #ifndef PMC_TREES_CAP
 #define PMC_TREES_CAP 84
