@@ -191,6 +191,11 @@ int pmc_store_put_batch(pmc_store *s, const uint8_t *src, const uint64_t *src_of
 /* Decompress extents into framed responses (frame = PMC_FRAME_*): resp[i], resp_len[i], rc[i]. */
 int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n, int frame, const uint8_t **resp,
                         uint32_t *resp_len, int32_t *rc);
+/* The same with a frame per extent (frames[i] = PMC_FRAME_*): one batch answers connections of
+ * both protocols, as one epoll iteration of the reference server does (server.cpp:434-478 frames
+ * custom and RESP requests side by side; responses at protocol.cpp:399-406 and :466-497). */
+int pmc_store_get_batch_frames(pmc_store *s, const pmc_extent *ext, uint32_t n, const uint8_t *frames,
+                               const uint8_t **resp, uint32_t *resp_len, int32_t *rc);
 /* Copy extents' compressed bytes (gzip members) to host memory: member i at dst + dst_off[i]. */
 int pmc_store_read_members(pmc_store *s, const pmc_extent *ext, uint32_t n, uint8_t *dst,
                            const uint64_t *dst_off);

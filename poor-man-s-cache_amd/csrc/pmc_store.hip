@@ -237,10 +237,10 @@ PMC_API int pmc_store_put_batch(pmc_store *s, const uint8_t *src, const uint64_t
     return PMC_OK;
 }
 
-PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n, int frame, const uint8_t **resp,
-                                uint32_t *resp_len, int32_t *rc) {
-    if (!s || (n && (!ext || !resp || !resp_len || !rc)) || frame < PMC_FRAME_RAW || frame > PMC_FRAME_RESP)
-        return PMC_E_ARG;
+// frame_of(i): extent i's PMC_FRAME_* (checked by the callers)
+template <class FrameOf>
+static int store_get(pmc_store *s, const pmc_extent *ext, uint32_t n, FrameOf frame_of, const uint8_t **resp,
+                     uint32_t *resp_len, int32_t *rc) {
     if (n == 0) return PMC_OK;
     StoreCall call(s, s->get_mu);
     pmc_ctx *ctx = s->ctx;
@@ -256,8 +256,9 @@ PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n,
         }
         return d;
     };
-    const uint32_t tl = frame == PMC_FRAME_RESP ? 2 : frame == PMC_FRAME_CUSTOM ? 1 : 0;
+    auto tail = [](int frame) -> uint32_t { return frame == PMC_FRAME_RESP ? 2 : frame == PMC_FRAME_CUSTOM ? 1 : 0; };
     for (uint32_t i = 0; i < n; i++) {
+        const int frame = frame_of(i);
         resp[i] = nullptr;
         resp_len[i] = 0;
         if (!(ext[i].flags & 1) || ext[i].len == 0) {
@@ -266,7 +267,7 @@ PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n,
         }
         hlen[i] = (uint8_t)(frame == PMC_FRAME_RESP ? 1 + digits(ext[i].raw_len) + 2 : 0);
         pos[i] = total;
-        total += hlen[i] + (uint64_t)ext[i].raw_len + tl;
+        total += hlen[i] + (uint64_t)ext[i].raw_len + tail(frame);
         max_raw = std::max<uint64_t>(max_raw, ext[i].raw_len);
         rc[i] = PMC_OK;
         pick.push_back(i);
@@ -310,6 +311,7 @@ PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n,
             rc[i] = h_rc[k] != PMC_OK ? h_rc[k] : PMC_Z_DATA_ERROR;
             continue;
         }
+        const int frame = frame_of(i);
         uint8_t *p = img + pos[i];
         if (frame == PMC_FRAME_RESP) {  // "$<len>\r\n" value "\r\n"  (protocol.cpp:466-497)
             const int nd = hlen[i] - 3;
@@ -327,9 +329,24 @@ PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n,
             p[ext[i].raw_len] = 0x1F;
         }
         resp[i] = p;
-        resp_len[i] = hlen[i] + ext[i].raw_len + tl;
+        resp_len[i] = hlen[i] + ext[i].raw_len + tail(frame);
     }
     return PMC_OK;
+}
+
+PMC_API int pmc_store_get_batch(pmc_store *s, const pmc_extent *ext, uint32_t n, int frame, const uint8_t **resp,
+                                uint32_t *resp_len, int32_t *rc) {
+    if (!s || (n && (!ext || !resp || !resp_len || !rc)) || frame < PMC_FRAME_RAW || frame > PMC_FRAME_RESP)
+        return PMC_E_ARG;
+    return store_get(s, ext, n, [frame](uint32_t) { return frame; }, resp, resp_len, rc);
+}
+
+PMC_API int pmc_store_get_batch_frames(pmc_store *s, const pmc_extent *ext, uint32_t n, const uint8_t *frames,
+                                       const uint8_t **resp, uint32_t *resp_len, int32_t *rc) {
+    if (!s || (n && (!ext || !frames || !resp || !resp_len || !rc))) return PMC_E_ARG;
+    for (uint32_t i = 0; i < n; i++)
+        if (frames[i] > PMC_FRAME_RESP) return PMC_E_ARG;
+    return store_get(s, ext, n, [frames](uint32_t i) { return (int)frames[i]; }, resp, resp_len, rc);
 }
 
 PMC_API int pmc_store_read_members(pmc_store *s, const pmc_extent *ext, uint32_t n, uint8_t *dst,

@@ -64,6 +64,7 @@ SIGNATURES = {
     "pmc_store_destroy": (None, [_p]),
     "pmc_store_put_batch": (_c.c_int, [_p, _p, _p, _p, _u32, _p, _p]),
     "pmc_store_get_batch": (_c.c_int, [_p, _p, _u32, _c.c_int, _p, _p, _p]),
+    "pmc_store_get_batch_frames": (_c.c_int, [_p, _p, _u32, _p, _p, _p, _p]),
     "pmc_store_read_members": (_c.c_int, [_p, _p, _u32, _p, _p]),
     "pmc_store_free": (_c.c_int, [_p, _p, _u32]),
     "pmc_store_stats": (_c.c_int, [_p, _c.POINTER(_u64), _c.POINTER(_u64), _c.POINTER(_u64)]),
@@ -370,7 +371,8 @@ class Store:
         return ext, [int(x) for x in rc[:n]]
 
     def get(self, ext, n=None, frame=FRAME_RAW):
-        """-> list of (rc, response bytes)."""
+        """-> list of (rc, response bytes).  frame: one FRAME_* for the batch, or a sequence of n
+        (pmc_store_get_batch_frames)."""
         import numpy as np
         n = len(ext) if n is None else n
         if n == 0:
@@ -378,7 +380,13 @@ class Store:
         resp = (_p * n)()
         rlen = np.zeros(n, dtype=np.uint32)
         rc = np.zeros(n, dtype=np.int32)
-        r = lib().pmc_store_get_batch(self.handle, ext, n, frame, resp, rlen.ctypes.data, rc.ctypes.data)
+        if isinstance(frame, int):
+            r = lib().pmc_store_get_batch(self.handle, ext, n, frame, resp, rlen.ctypes.data, rc.ctypes.data)
+        else:
+            fr = np.ascontiguousarray(frame, dtype=np.uint8)
+            assert fr.shape == (n,), fr.shape
+            r = lib().pmc_store_get_batch_frames(self.handle, ext, n, fr.ctypes.data, resp, rlen.ctypes.data,
+                                                 rc.ctypes.data)
         if r != 0:
             raise CodecUnavailable(f"pmc_store_get_batch = {r}: {last_error()}")
         return [(int(rc[i]), ctypes.string_at(resp[i], int(rlen[i])) if rc[i] == 0 else b"") for i in range(n)]

@@ -8,6 +8,8 @@
 //
 // usage: pmc_loadgen --port P --data DIR [--conns 16] [--keys 65536] [--vlen 4096] [--batch 100]
 //                    [--ops 200000] [--mix 50]       (percent of SETs in the timed phase)
+//                    [--proto custom|resp]           (resp: commands as RESP arrays, as the reference's
+//                                                     tcp_server_test.py --resp sends them through redis-py)
 // Phases: preload (SET every key once, untimed), then --ops timed commands over random keys,
 // every GET checked against the last value SET for its key.  Prints one JSON line.
 #include <arpa/inet.h>
@@ -45,7 +47,9 @@ struct Opts {
     int port = 9001, conns = 16, batch = 100, mix = 50, warmup_sec = 60;
     uint64_t keys = 65536, vlen = 4096, ops = 200000;
     std::string data;
+    bool resp = false;
 };
+bool g_resp = false;
 
 std::string corpus;
 
@@ -74,15 +78,39 @@ int connect_to(int port) {
 // server that answers the first requests of a batch before it has read the last ones (the reference
 // server sends each epoll iteration's responses before reading again, server.cpp:386-390, and spins on
 // EAGAIN until they are sent) would otherwise deadlock against a client still blocked in send().
+// One reply at pos: custom replies end at 0x1F (kept out of the reply), RESP replies are a "+ - :" line or a
+// "$<len>\r\n" bulk string (kept whole).  Returns the reply's end (npos: incomplete); *next: past it.
+size_t reply_end(const std::string &b, size_t pos, size_t *next) {
+    if (!g_resp) {
+        const size_t e = b.find('\x1f', pos);
+        if (e != std::string::npos) *next = e + 1;
+        return e;
+    }
+    const size_t e = b.find("\r\n", pos);
+    if (e == std::string::npos) return e;
+    if (b[pos] != '$' || b[pos + 1] == '-') return *next = e + 2;
+    const size_t end = e + 2 + strtoull(b.c_str() + pos + 1, nullptr, 10) + 2;
+    if (b.size() < end) return std::string::npos;
+    return *next = end;
+}
+
+std::string bulk(const std::string &v) { return "$" + std::to_string(v.size()) + "\r\n" + v + "\r\n"; }
+std::string resp_cmd(std::initializer_list<const std::string *> parts) {
+    std::string r = "*" + std::to_string(parts.size()) + "\r\n";
+    for (const std::string *p : parts) r += bulk(*p);
+    return r;
+}
+
 bool exchange(int fd, const std::string &req, std::string &buf, size_t n, std::vector<std::string> &out) {
     out.clear();
     size_t sent = 0, pos = 0;
     char tmp[1 << 16];
     while (out.size() < n) {
-        const size_t e = buf.find('\x1f', pos);
+        size_t next = 0;
+        const size_t e = pos < buf.size() ? reply_end(buf, pos, &next) : std::string::npos;
         if (e != std::string::npos) {
             out.emplace_back(buf, pos, e - pos);
-            pos = e + 1;
+            pos = next;
             continue;
         }
         buf.erase(0, pos);
@@ -122,7 +150,8 @@ bool warm_up(int port, int secs) {
         const int fd = connect_to(port);
         if (fd >= 0) {
             pollfd pf{fd, POLLOUT, 0};
-            const std::string req = "GET __warmup__\x1f";
+            static const std::string wk = "__warmup__", get = "GET";
+            const std::string req = g_resp ? resp_cmd({&get, &wk}) : "GET __warmup__\x1f";
             bool ok = send(fd, req.data(), req.size(), MSG_NOSIGNAL) == (ssize_t)req.size();
             pf.events = POLLIN;
             ok = ok && poll(&pf, 1, 1000) > 0 && (pf.revents & POLLIN);
@@ -155,6 +184,7 @@ int main(int argc, char **argv) {
         else if (a == "--mix") o.mix = atoi(v.c_str());
         else if (a == "--data") o.data = v;
         else if (a == "--warmup-sec") o.warmup_sec = atoi(v.c_str());
+        else if (a == "--proto") o.resp = g_resp = v == "resp";
         else {
             fprintf(stderr, "unknown option %s\n", a.c_str());
             return 2;
@@ -220,14 +250,17 @@ int main(int argc, char **argv) {
                             set = (int)((rng >> 40) % 100) < o.mix;
                         }
                         const uint64_t k = mine[ki];
+                        static const std::string kSet = "SET", kGet = "GET";
+                        const std::string key = "key" + std::to_string(k);
                         if (set) {
                             const std::string v = value_of(k, ++ver[ki], o.vlen);
-                            req += "SET key" + std::to_string(k) + " " + v + '\x1f';
-                            expect.emplace_back(0, "OK");
+                            req += o.resp ? resp_cmd({&kSet, &key, &v}) : "SET " + key + " " + v + '\x1f';
+                            expect.emplace_back(0, o.resp ? "+OK\r\n" : "OK");
                             me.sets++;
                         } else {
-                            req += "GET key" + std::to_string(k) + '\x1f';
-                            expect.emplace_back(1, value_of(k, ver[ki], o.vlen));
+                            req += o.resp ? resp_cmd({&kGet, &key}) : "GET " + key + '\x1f';
+                            const std::string v = value_of(k, ver[ki], o.vlen);
+                            expect.emplace_back(1, o.resp ? bulk(v) : v);
                             me.gets++;
                         }
                         me.bytes += o.vlen;
@@ -264,9 +297,9 @@ int main(int argc, char **argv) {
     }
     printf("{\"ops\": %llu, \"sets\": %llu, \"gets\": %llu, \"seconds\": %.4f, \"ops_per_s\": %.1f, "
            "\"value_gib_s\": %.4f, \"mismatches\": %llu, \"failed_conns\": %d, \"conns\": %d, \"batch\": %d, "
-           "\"vlen\": %llu, \"keys\": %llu, \"set_pct\": %d}\n",
+           "\"vlen\": %llu, \"keys\": %llu, \"set_pct\": %d, \"proto\": \"%s\"}\n",
            (unsigned long long)s.ops, (unsigned long long)s.sets, (unsigned long long)s.gets, t, s.ops / t,
            s.bytes / t / (1ull << 30), (unsigned long long)s.bad, failed.load(), o.conns, o.batch,
-           (unsigned long long)o.vlen, (unsigned long long)o.keys, o.mix);
+           (unsigned long long)o.vlen, (unsigned long long)o.keys, o.mix, o.resp ? "resp" : "custom");
     return (s.bad || failed) ? 1 : 0;
 }

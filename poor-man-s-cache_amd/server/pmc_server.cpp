@@ -12,15 +12,19 @@
 //      compressed iff compression is on and strlen + 1 >= 30 (kvs.hpp:26, kvs.cpp:182); a GET that
 //      follows a SET of the same key in the iteration answers with that SET's value (no codec);
 //   3. run the iteration's compressions as ONE pmc_store_put_batch per GPU (values go to HBM
-//      extents, f2) and its decompressions of stored values as ONE pmc_store_get_batch per GPU,
-//      framed as value + 0x1F straight into a pinned send image (f3); GPUs run on their own threads
+//      extents, f2) and its decompressions of stored values as ONE pmc_store_get_batch_frames per GPU,
+//      framed as value + 0x1F or a RESP bulk string straight into a pinned send image (f3); GPUs run on their own threads
 //      (shard = hashFunc(key) % shards, GPU = shard % nGPU: server.cpp:113,121,132 and SURVEY §8e);
 //   4. send each connection's responses in request order with one sendmsg (iovecs point into the
 //      pinned image, the request buffers and static strings: no value is copied on the host).
 // A failed compression stores the raw value (kvs.cpp:188-192); extents replaced or deleted during
 // an iteration are released after its GETs ran.  --codec single instead calls the single-value
 // C-ABI (what the unchanged server does through the drop-in GzipCompressor), --codec off stores
-// raw values (ENABLE_COMPRESSION=false).  Custom protocol only (RESP is out of scope).
+// raw values (ENABLE_COMPRESSION=false).
+// Both of the reference's protocols: custom requests end at 0x1F; RESP arrays ("*<n>\r\n" + bulk strings,
+// GET/SET/DEL and MULTI/EXEC/DISCARD transactions, server.cpp:147-280) are framed by their lengths
+// (protocol.cpp:294-356) and answered as RESP (protocol.cpp:399-567): a stored value's bulk string
+// "$<len>\r\n<value>\r\n" is framed in the same device batch as the custom GETs (per-extent frames).
 //
 // usage: pmc_server --port P [--gpus N] [--shards 128] [--codec batch|single|off] [--heap-mb M]
 //        prints "READY <port>" once listening; SIGTERM/SIGINT -> one JSON stats line, exit 0.
@@ -60,11 +64,31 @@ const char kInternal[] = "ERROR: Internal error";
 const char kUnknown[] = "ERROR: Unknown command";
 const char kUnparsable[] = "ERROR: Unable to parse request";
 const char kBadFormat[] = "ERROR: Invalid command format";
+// RESP payloads (protocol.cpp:36-48, protocol.hpp:24-25): errors are "-ERR " + message + CRLF
+const char kRespOK[] = "+OK\r\n";
+const char kRespQueued[] = "+QUEUED\r\n";
+const char kRespNil[] = "$-1\r\n";
+const char kRespOne[] = ":1\r\n";
+const char kRespZero[] = ":0\r\n";
+const char kRespErrNested[] = "-ERR ERR MULTI calls can not be nested\r\n";
+const char kRespErrExecNoMulti[] = "-ERR ERR EXEC without MULTI\r\n";
+const char kRespErrDiscardNoMulti[] = "-ERR ERR DISCARD without MULTI\r\n";
+const char kRespErrExecAborted[] = "-ERR EXECABORT Transaction discarded because of previous errors.\r\n";
+const char kRespErrUnknown[] = "-ERR ERROR: Unknown command\r\n";
+const char kRespErrUnparsable[] = "-ERR ERROR: Unable to parse request\r\n";
+const char kRespErrBadFormat[] = "-ERR ERROR: Invalid command format\r\n";
 
 volatile sig_atomic_t g_stop = 0;
 void on_signal(int) { g_stop = 1; }
 
 enum class Codec { kBatch, kSingle, kOff };
+
+enum : uint8_t { kCustom = 0, kResp = 1 };
+enum : uint8_t { kGet, kSet, kDel };
+struct TxCmd {  // a command queued by MULTI (RespTransactionState, persisted strings: server.cpp:161-173)
+    uint8_t type;
+    std::string key, val;
+};
 
 struct Conn {
     int fd = -1;
@@ -72,6 +96,8 @@ struct Conn {
     size_t parsed = 0;  // bytes framed into requests so far
     std::string out;    // response bytes a previous sendmsg could not take
     bool closing = false;
+    bool tx_active = false, tx_aborted = false;  // RESP MULTI state (server.cpp:148-159)
+    std::vector<TxCmd> tx;
 };
 
 enum : uint8_t { kRaw = 0, kDevice = 1, kHostGz = 2, kPending = 3 };
@@ -87,6 +113,7 @@ struct Entry {
 enum : uint8_t { kStatic, kArena, kView, kStoreGet };
 struct Resp {
     uint8_t kind = kStatic;
+    uint8_t proto = kCustom;  // kCustom: + 0x1F on the wire; kResp: the bytes are the whole RESP reply
     uint32_t gpu = 0;
     const char *p = nullptr;  // kStatic / kView
     size_t off = 0, n = 0;    // kArena: offset + length; kStoreGet: index in gets[gpu]
@@ -105,6 +132,7 @@ struct Gpu {
     pmc_store *store = nullptr;
     std::vector<Put> puts;
     std::vector<pmc_extent> put_ext, gets, to_free;
+    std::vector<uint8_t> get_frame;  // PMC_FRAME_CUSTOM / PMC_FRAME_RESP per get
     std::vector<int32_t> put_rc, get_rc;
     std::vector<const uint8_t *> get_resp;
     std::vector<uint32_t> get_len;
@@ -112,7 +140,7 @@ struct Gpu {
 };
 
 struct Stats {
-    uint64_t iterations = 0, requests = 0, sets = 0, gets = 0, dels = 0, compressed = 0, decompressed = 0,
+    uint64_t iterations = 0, requests = 0, resp_requests = 0, sets = 0, gets = 0, dels = 0, compressed = 0, decompressed = 0,
              raw_fallbacks = 0, pending_hits = 0, put_calls = 0, get_calls = 0;
     double t_codec = 0, t_put = 0, t_get = 0, t_iter = 0;  // seconds: codec phase, store calls, whole iterations
 };
@@ -133,12 +161,23 @@ class Server {
     std::unordered_map<int, std::unique_ptr<Conn>> conns;
     std::vector<Req> reqs;
     std::string arena;
+    std::vector<std::vector<TxCmd>> tx_keep;  // EXEC'd queues: puts and views point into them this iteration
 
     void accept_all();
     void read_conn(Conn *c);
     void frame(Conn *c);
     void process();
-    void apply(Req &q, std::string_view payload);
+    void apply(size_t q, std::string_view payload);
+    void apply_resp(Conn *c, size_t q, std::string_view payload);
+    void do_set(Resp &r, std::string_view key, std::string_view val);
+    void do_get(Resp &r, std::string_view key);
+    void do_del(Resp &r, std::string_view key);
+    size_t push_req(Conn *c, uint8_t proto) {
+        reqs.push_back(Req{c, Resp{}});
+        reqs.back().r.proto = proto;
+        return reqs.size() - 1;
+    }
+    void resp_bulk_arena(Resp &r, const char *p, size_t n);
     void run_codec();
     void send_conn(Conn *c, size_t first, size_t last);
     void flush(Conn *c);
@@ -211,9 +250,11 @@ int Server::run(int port) {
         // one batch: every complete request of every ready connection
         reqs.clear();
         arena.clear();
+        tx_keep.clear();
         for (auto &g : gpus) {
             g.puts.clear();
             g.gets.clear();
+            g.get_frame.clear();
         }
         std::vector<std::pair<size_t, size_t>> span(ready.size());
         for (size_t j = 0; j < ready.size(); j++) {
@@ -236,11 +277,12 @@ int Server::run(int port) {
         st.iterations++;
         st.t_iter += now_s() - t_it;
     }
-    printf("{\"iterations\": %llu, \"requests\": %llu, \"sets\": %llu, \"gets\": %llu, \"dels\": %llu, "
+    printf("{\"iterations\": %llu, \"requests\": %llu, \"resp_requests\": %llu, \"sets\": %llu, \"gets\": %llu, \"dels\": %llu, "
            "\"compressed\": %llu, \"decompressed\": %llu, \"raw_fallbacks\": %llu, \"pending_hits\": %llu, "
            "\"put_calls\": %llu, \"get_calls\": %llu, \"t_iter\": %.4f, \"t_codec\": %.4f, \"t_put\": %.4f, "
            "\"t_get\": %.4f}\n",
-           (unsigned long long)st.iterations, (unsigned long long)st.requests, (unsigned long long)st.sets,
+           (unsigned long long)st.iterations, (unsigned long long)st.requests,
+           (unsigned long long)st.resp_requests, (unsigned long long)st.sets,
            (unsigned long long)st.gets, (unsigned long long)st.dels, (unsigned long long)st.compressed,
            (unsigned long long)st.decompressed, (unsigned long long)st.raw_fallbacks,
            (unsigned long long)st.pending_hits, (unsigned long long)st.put_calls, (unsigned long long)st.get_calls,
@@ -281,24 +323,90 @@ void Server::read_conn(Conn *c) {
     }
 }
 
-// custom protocol: requests end at 0x1F; empty ones are skipped (server.cpp:438-478)
-void Server::frame(Conn *c) {
-    size_t pos = c->parsed;
-    for (;;) {
-        while (pos < c->in.size() && c->in[pos] == kSep) pos++;
-        const size_t end = c->in.find(kSep, pos);
-        if (end == std::string::npos) break;
-        reqs.push_back(Req{c, Resp{}});
-        apply(reqs.back(), std::string_view(c->in.data() + pos, end - pos));
-        pos = end + 1;
+// RESP framing (parseRespMessageLength, protocol.cpp:294-356): "*<n>\r\n" then n bulk strings
+// "$<len>\r\n<bytes>\r\n".  Returns the message length, 0 = incomplete, SIZE_MAX = malformed.
+size_t resp_message_length(const char *b, size_t start, size_t end) {
+    size_t idx = start + 1;
+    auto number = [&](size_t &out) -> int {  // 1 ok, 0 incomplete, -1 error
+        size_t v = 0;
+        bool any = false;
+        while (idx < end) {
+            const char c = b[idx];
+            if (c == '\r') {
+                if (idx + 1 >= end || b[idx + 1] != '\n' || !any) return -1;  // (the reference: Error here)
+                idx += 2;
+                out = v;
+                return 1;
+            }
+            if (c < '0' || c > '9') return -1;
+            any = true;
+            v = v * 10 + (size_t)(c - '0');
+            idx++;
+        }
+        return any ? 0 : -1;  // (protocol.cpp:321: no digit before the end is an Error, digits are not)
+    };
+    size_t n = 0;
+    int k = number(n);
+    if (k <= 0) return k < 0 ? SIZE_MAX : 0;
+    for (size_t a = 0; a < n; a++) {
+        if (idx >= end) return 0;
+        if (b[idx] != '$') return SIZE_MAX;
+        idx++;
+        size_t len = 0;
+        k = number(len);
+        if (k <= 0) return k < 0 ? SIZE_MAX : 0;
+        if (idx + len + 2 > end) return 0;
+        idx += len;
+        if (b[idx] != '\r' || b[idx + 1] != '\n') return SIZE_MAX;
+        idx += 2;
     }
-    c->parsed = pos;
+    return idx - start;
 }
 
-// one request, in order, against the index (processRequestSync server.cpp:278-321 + kvs semantics)
-void Server::apply(Req &q, std::string_view payload) {
+// custom requests end at 0x1F, empty ones are skipped; a '*' starts a RESP array (readRequestAsync,
+// server.cpp:433-479).  A malformed RESP array closes the connection and drops every request framed from
+// this read (server.cpp:448-455): so the whole read is framed before any request is applied.
+void Server::frame(Conn *c) {
+    struct Span {
+        size_t pos, len;
+        uint8_t proto;
+    };
+    std::vector<Span> spans;
+    size_t pos = c->parsed;
+    const char *b = c->in.data();
+    const size_t end = c->in.size();
+    for (;;) {
+        while (pos < end && b[pos] == kSep) pos++;
+        if (pos >= end) break;
+        if (b[pos] == '*') {
+            const size_t n = resp_message_length(b, pos, end);
+            if (n == 0) break;
+            if (n == SIZE_MAX) {
+                c->closing = true;
+                c->parsed = end;
+                return;
+            }
+            spans.push_back(Span{pos, n, kResp});
+            pos += n;
+            continue;
+        }
+        const size_t e = c->in.find(kSep, pos);
+        if (e == std::string::npos) break;
+        spans.push_back(Span{pos, e - pos, kCustom});
+        pos = e + 1;
+    }
+    c->parsed = pos;
+    for (const Span &sp : spans) {
+        const std::string_view payload(b + sp.pos, sp.len);
+        if (sp.proto == kResp) apply_resp(c, push_req(c, kResp), payload);
+        else apply(push_req(c, kCustom), payload);
+    }
+}
+
+// one custom request, in order, against the index (processRequestSync server.cpp:282-321)
+void Server::apply(size_t q, std::string_view payload) {
     st.requests++;
-    Resp &r = q.r;
+    Resp &r = reqs[q].r;
     r.kind = kStatic;
     const size_t sp1 = payload.find(' ');
     if (sp1 == std::string_view::npos) {
@@ -318,94 +426,212 @@ void Server::apply(Req &q, std::string_view payload) {
             r.p = kBadFormat;
             return;
         }
-        st.sets++;
-        std::string_view val = rest.substr(sp2 + 1);
-        val = val.substr(0, strnlen(val.data(), val.size()));  // a C string (kvs.cpp:148 strlen)
-        const uint32_t g = gpu_of(key);
-        Entry &e = shard_of(key)[std::string(key)];
-        if (e.kind == kDevice) gpus[e.gpu].to_free.push_back(e.ext);
-        e.gpu = g;
-        if (codec != Codec::kOff && val.size() + 1 >= kMinCompress) {
-            if (codec == Codec::kBatch) {
-                e.kind = kPending;
-                std::string().swap(e.bytes);  // an earlier raw / host-gzip value leaves host memory
-                e.put = (uint32_t)gpus[g].puts.size();
-                gpus[g].puts.push_back(Put{key, val});
-            } else {  // single-value call, as the unchanged server through the drop-in
-                e.bytes.resize(pmc_gzip_bound(val.size()));
-                size_t n = 0;
-                if (pmc_gzip_compress(gpus[g].ctx, val.data(), val.size(), e.bytes.data(), e.bytes.size(), &n) == 0) {
-                    e.bytes.resize(n);
-                    e.kind = kHostGz;
-                    st.compressed++;
-                } else {
-                    e.bytes.assign(val.data(), val.size());
-                    e.kind = kRaw;
-                    st.raw_fallbacks++;
-                }
-            }
-        } else {
-            e.kind = kRaw;
-            e.bytes.assign(val.data(), val.size());
-        }
-        r.p = kOK;
+        do_set(r, key, rest.substr(sp2 + 1));
         return;
     }
-    if (cmd == "GET") {
-        st.gets++;
-        auto &m = shard_of(key);
-        auto it = m.find(std::string(key));
-        if (it == m.end()) {
-            r.p = kNil;
-            return;
-        }
-        Entry &e = it->second;
-        if (e.kind == kRaw) {  // copied: a later SET in this iteration may replace it
-            r.kind = kArena;
-            r.n = e.bytes.size();
-            r.off = put_arena(e.bytes.data(), r.n);
-        } else if (e.kind == kPending) {  // SET earlier in this iteration: its own bytes
-            r.kind = kView;
-            r.p = gpus[e.gpu].puts[e.put].val.data();
-            r.n = gpus[e.gpu].puts[e.put].val.size();
-            st.pending_hits++;
-        } else if (e.kind == kDevice) {
-            r.kind = kStoreGet;
-            r.gpu = e.gpu;
-            r.off = gpus[e.gpu].gets.size();
-            gpus[e.gpu].gets.push_back(e.ext);
-        } else {  // kHostGz: single-value decompress now
-            const uint32_t cap = pmc_gzip_isize(e.bytes.data(), e.bytes.size());
-            const size_t o = arena.size();
-            arena.resize(o + cap + 1);
-            size_t n = 0;
-            if (pmc_gzip_decompress(gpus[e.gpu].ctx, e.bytes.data(), e.bytes.size(), &arena[o], cap + 1, &n) == 0) {
-                arena.resize(o + n);
-                r.kind = kArena;
-                r.off = o;
-                r.n = n;
-                st.decompressed++;
-            } else {
-                arena.resize(o);
-                r.p = kNil;  // decompressEntry's nullptr (kvs.cpp:234) -> NOTHING (shard.cpp:30)
-            }
-        }
-        return;
-    }
-    if (cmd == "DEL") {
-        st.dels++;
-        auto &m = shard_of(key);
-        auto it = m.find(std::string(key));
-        if (it == m.end()) {
-            r.p = kKeyNotExists;
-            return;
-        }
-        if (it->second.kind == kDevice) gpus[it->second.gpu].to_free.push_back(it->second.ext);
-        m.erase(it);  // a pending put of this key is released once it ran (run_codec)
-        r.p = kOK;
-        return;
-    }
+    if (cmd == "GET") return do_get(r, key);
+    if (cmd == "DEL") return do_del(r, key);
     r.p = kUnknown;
+}
+
+// one RESP request (processRequestSync server.cpp:147-280; parseRespCommand protocol.cpp:358-397)
+void Server::apply_resp(Conn *c, size_t q, std::string_view payload) {
+    st.requests++;
+    st.resp_requests++;
+    reqs[q].r.kind = kStatic;
+    auto fail = [&](const char *err) {  // ++numErrors; markRespTransactionError
+        if (c->tx_active) c->tx_aborted = true;
+        reqs[q].r.p = err;
+    };
+    // parts: 1-3 bulk strings; each is a C string to the reference (it writes a NUL at its CR)
+    std::string_view part[3];
+    size_t argc = 0, idx = 1;
+    const char *b = payload.data();
+    const size_t end = payload.size();
+    auto number = [&](size_t &out) {
+        size_t v = 0;
+        bool any = false;
+        while (idx < end && b[idx] >= '0' && b[idx] <= '9') v = v * 10 + (size_t)(b[idx++] - '0'), any = true;
+        if (!any || idx + 1 >= end || b[idx] != '\r' || b[idx + 1] != '\n') return false;
+        idx += 2;
+        out = v;
+        return true;
+    };
+    bool ok = number(argc) && argc >= 1 && argc <= 3;
+    for (size_t i = 0; ok && i < argc; i++) {
+        size_t len = 0;
+        ok = idx < end && b[idx++] == '$' && number(len) && idx + len + 2 <= end;
+        if (ok) {
+            part[i] = std::string_view(b + idx, strnlen(b + idx, len));
+            idx += len + 2;
+        }
+    }
+    if (!ok) return fail(kRespErrUnparsable);
+    const std::string_view cmd = part[0];
+    Resp &r = reqs[q].r;
+    if (cmd == "MULTI") {
+        if (c->tx_active) return fail(kRespErrNested);
+        c->tx_active = true;
+        c->tx_aborted = false;
+        c->tx.clear();
+        r.p = kRespOK;
+        return;
+    }
+    if (cmd == "DISCARD") {
+        if (!c->tx_active) {
+            r.p = kRespErrDiscardNoMulti;
+            return;
+        }
+        c->tx.clear();
+        c->tx_active = c->tx_aborted = false;
+        r.p = kRespOK;
+        return;
+    }
+    if (cmd == "EXEC") {
+        if (!c->tx_active) {
+            r.p = kRespErrExecNoMulti;
+            return;
+        }
+        const bool aborted = c->tx_aborted;
+        c->tx_active = c->tx_aborted = false;
+        if (aborted) {
+            c->tx.clear();
+            r.p = kRespErrExecAborted;
+            return;
+        }
+        // makeRespArray (protocol.cpp:499-533): "*<n>\r\n" and the n replies, each its own Resp here
+        tx_keep.push_back(std::move(c->tx));
+        c->tx.clear();
+        const std::vector<TxCmd> &queue = tx_keep.back();
+        char hdr[32];
+        const int hn = snprintf(hdr, sizeof hdr, "*%zu\r\n", queue.size());
+        r.kind = kArena;
+        r.n = (size_t)hn;
+        r.off = put_arena(hdr, r.n);
+        for (const TxCmd &t : queue) {
+            const size_t e = push_req(c, kResp);
+            Resp &er = reqs[e].r;
+            er.kind = kStatic;
+            if (t.type == kGet) do_get(er, t.key);
+            else if (t.type == kSet) do_set(er, t.key, t.val);
+            else do_del(er, t.key);
+        }
+        return;
+    }
+    const uint8_t type = cmd == "GET" ? kGet : cmd == "SET" ? kSet : cmd == "DEL" ? kDel : 0xFF;
+    if (type == 0xFF) return fail(kRespErrUnknown);
+    if (argc != (type == kSet ? 3u : 2u)) return fail(kRespErrBadFormat);
+    if (c->tx_active) {  // queueRespCommand
+        c->tx.push_back(TxCmd{type, std::string(part[1]), std::string(type == kSet ? part[2] : std::string_view())});
+        r.p = kRespQueued;
+        return;
+    }
+    if (type == kGet) do_get(r, part[1]);
+    else if (type == kSet) do_set(r, part[1], part[2]);
+    else do_del(r, part[1]);
+}
+
+// "$<len>\r\n" value "\r\n" into the arena (makeRespBulkString, protocol.cpp:466-497)
+void Server::resp_bulk_arena(Resp &r, const char *p, size_t n) {
+    char hdr[32];
+    const int hn = snprintf(hdr, sizeof hdr, "$%zu\r\n", n);
+    r.kind = kArena;
+    r.off = put_arena(hdr, (size_t)hn);
+    put_arena(p, n);
+    put_arena("\r\n", 2);
+    r.n = (size_t)hn + n + 2;
+}
+
+// SET / GET / DEL against the index (KeyValueStore semantics, kvs.cpp:141-235); r.proto picks the reply
+void Server::do_set(Resp &r, std::string_view key, std::string_view val) {
+    st.sets++;
+    val = val.substr(0, strnlen(val.data(), val.size()));  // a C string (kvs.cpp:148 strlen)
+    const uint32_t g = gpu_of(key);
+    Entry &e = shard_of(key)[std::string(key)];
+    if (e.kind == kDevice) gpus[e.gpu].to_free.push_back(e.ext);
+    e.gpu = g;
+    if (codec != Codec::kOff && val.size() + 1 >= kMinCompress) {
+        if (codec == Codec::kBatch) {
+            e.kind = kPending;
+            std::string().swap(e.bytes);  // an earlier raw / host-gzip value leaves host memory
+            e.put = (uint32_t)gpus[g].puts.size();
+            gpus[g].puts.push_back(Put{key, val});
+        } else {  // single-value call, as the unchanged server through the drop-in
+            e.bytes.resize(pmc_gzip_bound(val.size()));
+            size_t n = 0;
+            if (pmc_gzip_compress(gpus[g].ctx, val.data(), val.size(), e.bytes.data(), e.bytes.size(), &n) == 0) {
+                e.bytes.resize(n);
+                e.kind = kHostGz;
+                st.compressed++;
+            } else {
+                e.bytes.assign(val.data(), val.size());
+                e.kind = kRaw;
+                st.raw_fallbacks++;
+            }
+        }
+    } else {
+        e.kind = kRaw;
+        e.bytes.assign(val.data(), val.size());
+    }
+    r.p = r.proto == kResp ? kRespOK : kOK;
+}
+
+void Server::do_get(Resp &r, std::string_view key) {
+    st.gets++;
+    const bool resp = r.proto == kResp;
+    auto &m = shard_of(key);
+    auto it = m.find(std::string(key));
+    if (it == m.end()) {
+        r.p = resp ? kRespNil : kNil;
+        return;
+    }
+    Entry &e = it->second;
+    if (e.kind == kRaw) {  // copied: a later SET in this iteration may replace it
+        if (resp) return resp_bulk_arena(r, e.bytes.data(), e.bytes.size());
+        r.kind = kArena;
+        r.n = e.bytes.size();
+        r.off = put_arena(e.bytes.data(), r.n);
+    } else if (e.kind == kPending) {  // SET earlier in this iteration: its own bytes
+        const Put &pt = gpus[e.gpu].puts[e.put];
+        st.pending_hits++;
+        if (resp) return resp_bulk_arena(r, pt.val.data(), pt.val.size());
+        r.kind = kView;
+        r.p = pt.val.data();
+        r.n = pt.val.size();
+    } else if (e.kind == kDevice) {
+        r.kind = kStoreGet;
+        r.gpu = e.gpu;
+        r.off = gpus[e.gpu].gets.size();
+        gpus[e.gpu].gets.push_back(e.ext);
+        gpus[e.gpu].get_frame.push_back(resp ? PMC_FRAME_RESP : PMC_FRAME_CUSTOM);
+    } else {  // kHostGz: single-value decompress now
+        const uint32_t cap = pmc_gzip_isize(e.bytes.data(), e.bytes.size());
+        std::string v(cap + 1, '\0');
+        size_t n = 0;
+        if (pmc_gzip_decompress(gpus[e.gpu].ctx, e.bytes.data(), e.bytes.size(), v.data(), cap + 1, &n) == 0) {
+            st.decompressed++;
+            if (resp) return resp_bulk_arena(r, v.data(), n);
+            r.kind = kArena;
+            r.n = n;
+            r.off = put_arena(v.data(), n);
+        } else {
+            r.p = resp ? kRespNil : kNil;  // decompressEntry's nullptr (kvs.cpp:234) -> NOTHING (shard.cpp:30)
+        }
+    }
+}
+
+void Server::do_del(Resp &r, std::string_view key) {
+    st.dels++;
+    const bool resp = r.proto == kResp;
+    auto &m = shard_of(key);
+    auto it = m.find(std::string(key));
+    if (it == m.end()) {  // KEY_NOT_EXISTS; RESP: integer 0 (server.cpp:135-142)
+        r.p = resp ? kRespZero : kKeyNotExists;
+        return;
+    }
+    if (it->second.kind == kDevice) gpus[it->second.gpu].to_free.push_back(it->second.ext);
+    m.erase(it);  // a pending put of this key is released once it ran (run_codec)
+    r.p = resp ? kRespOne : kOK;
 }
 
 void Server::process() {
@@ -429,8 +655,8 @@ void Server::run_codec() {
             g.get_rc.assign(ng, 0);
             getter = std::thread([&] {
                 const double t0 = now_s();
-                gerr = pmc_store_get_batch(g.store, g.gets.data(), ng, PMC_FRAME_CUSTOM, g.get_resp.data(),
-                                           g.get_len.data(), g.get_rc.data());
+                gerr = pmc_store_get_batch_frames(g.store, g.gets.data(), ng, g.get_frame.data(), g.get_resp.data(),
+                                                  g.get_len.data(), g.get_rc.data());
                 if (&g == &gpus[0]) {
                     st.t_get += now_s() - t0;
                     st.get_calls++;
@@ -501,30 +727,29 @@ void Server::send_conn(Conn *c, size_t first, size_t last) {
     static const char sep = kSep;
     for (size_t i = first; i < last; i++) {
         const Resp &r = reqs[i].r;
+        const bool custom = r.proto == kCustom;  // RESP replies carry their own framing (server.cpp:555)
         switch (r.kind) {
         case kStatic:
             iov.push_back({(void *)r.p, strlen(r.p)});
-            iov.push_back({(void *)&sep, 1});
             break;
         case kArena:
             iov.push_back({(void *)(arena.data() + r.off), r.n});
-            iov.push_back({(void *)&sep, 1});
             break;
         case kView:
             iov.push_back({(void *)r.p, r.n});
-            iov.push_back({(void *)&sep, 1});
             break;
         case kStoreGet: {
             Gpu &g = gpus[r.gpu];
-            if (g.err || g.get_rc[r.off] != 0) {  // decompressEntry -> nullptr -> "(nil)"
-                iov.push_back({(void *)kNil, sizeof kNil - 1});
-                iov.push_back({(void *)&sep, 1});
-            } else {  // value + 0x1F, framed in the pinned image
+            if (g.err || g.get_rc[r.off] != 0) {  // decompressEntry -> nullptr -> "(nil)" / "$-1\r\n"
+                iov.push_back({(void *)(custom ? kNil : kRespNil), custom ? sizeof kNil - 1 : sizeof kRespNil - 1});
+            } else {  // value + 0x1F, or "$<len>\r\n" value "\r\n", framed in the pinned image
                 iov.push_back({(void *)g.get_resp[r.off], g.get_len[r.off]});
+                continue;
             }
             break;
         }
         }
+        if (custom) iov.push_back({(void *)&sep, 1});
     }
     size_t k = 0;
     if (c->out.empty()) {

@@ -12,6 +12,7 @@
 # 3.2.1: conn_manager.hpp:83-93, server.cpp:373,409).  A reference server that never answers has
 # self-deadlocked (validateConnections -> closeConnection relocks conn_mutex, conn_manager.hpp:117, :142;
 # about half of all starts on a long-running host): it is killed and started again, at most five times.
+# PROTO=resp sends every command as a RESP array (both servers speak it; server.cpp:147-280).
 #   OUT=gpurun_out/x bash scripts/ref_server_bench.sh
 cd "$GRAFT_REPO_ROOT" || cd "$(dirname "$0")/.." || exit 1
 OUT=${OUT:-gpurun_out/refsrv}
@@ -26,7 +27,7 @@ once() {  # tag cmd... : start a server (cmd), run the load, stop it
     # meanwhile are accepted together, inside the reference's connect race)
     for k in $(seq 1 600); do grep -q "ready to accept\|READY" "$OUT/server_$tag.log" 2>/dev/null && break; sleep 0.1; done
     timeout -k 5 240 $B/pmc_loadgen --port $port --data tests/golden/data --vlen $VLEN --ops $OPS --conns $CONNS \
-        --keys $KEYS --batch 100 --mix 50 --warmup-sec 10 > "$OUT/load_$tag.json" 2> "$OUT/load_$tag.err"
+        --keys $KEYS --batch 100 --mix 50 --warmup-sec 10 --proto ${PROTO:-custom} > "$OUT/load_$tag.json" 2> "$OUT/load_$tag.err"
     local rc=$?
     # (the no-codec leg: GET answers a pointer into the store, kvs.cpp:224, which a later SET of the same
     # key in the same epoll iteration frees before the responses go out -- a reference defect the codec
@@ -45,7 +46,7 @@ ref_server() { SERVER_PORT=$2 NUM_SHARDS=128 PMC_PRIME_STATS="$OUT/prime_$1_${VL
 ref_nocodec() { SERVER_PORT=$2 NUM_SHARDS=128 ENABLE_COMPRESSION=false oracle/_ref/ref_server_zlib; }
 pmc_srv() { $B/pmc_server --port $2 --codec $1 --heap-mb 8192; }
 case_() {  # label server-fn kind
-    local tag="$1_${VLEN}_${CONNS}_${KEYS}"
+    local tag="$1_${VLEN}_${CONNS}_${KEYS}_${PROTO:-custom}"
     for attempt in 1 2 3 4 5; do
         if once "$tag" $2 $3; then
             sed "s/^{/{\"server\": \"$1\", \"attempt\": $attempt, /" "$OUT/load_$tag.json" | tee -a "$OUT/ref_server_bench.jsonl"

@@ -35,6 +35,12 @@ def test_store_put_members_get_framed(ctx, golden):
         got = st.get(ext, len(pairs), frame)
         bad = [i for i, (r, _) in enumerate(pairs) if got[i] != (0, wrap(r))]
         assert not bad, (frame, bad[:10])
+    # one batch answering both protocols (pmc_store_get_batch_frames): frames cycle raw / custom / RESP
+    wraps = ((lambda v: v), (lambda v: v + b"\x1f"), (lambda v: b"$%d\r\n" % len(v) + v + b"\r\n"))
+    frames = [i % 3 for i in range(len(pairs))]
+    got = st.get(ext, len(pairs), frames)
+    bad = [i for i, (r, _) in enumerate(pairs) if got[i] != (0, wraps[frames[i]](r))]
+    assert not bad, bad[:10]
     s0 = st.stats()
     assert s0["used"] == s0["reserved"] > 0
 

@@ -23,7 +23,7 @@ import time
 
 import pytest
 
-from test_server import DATA, _exchange, _free_port, _load, _semantics
+from test_server import DATA, _exchange, _free_port, _load, _semantics, resp_malformed_closes, resp_semantics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF_BIN = os.path.join(ROOT, "oracle", "_ref")
@@ -232,6 +232,19 @@ def test_protocol_answers_equal_reference_server(golden, kind):
             _semantics(s.port, golden, one_by_one=True)
         finally:
             s.stop()
+
+
+def test_resp_answers_are_the_reference_servers(golden):
+    """test_server.resp_semantics's expected RESP replies (GET/SET/DEL, MULTI/EXEC/DISCARD, errors, custom
+    requests mixed in) are exactly what the reference server over zlib answers, and a malformed array closes
+    its connection the same way: the replies pmc_server is held to are pinned to the reference's.  One command
+    per write (raw values: see _semantics)."""
+    s = RefServer("zlib")
+    try:
+        resp_semantics(s.port, golden, one_by_one=True)
+        resp_malformed_closes(s.port)
+    finally:
+        s.stop()
 
 
 @pytest.mark.gpu
