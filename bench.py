@@ -46,6 +46,13 @@ def select_rank_keys(route, rank, n):
     return idx
 
 
+def landing_keys(route, world, n):
+    """bench.py --landing scatter: the batch that lands on one GPU holds every rank's keys (the first n routed to
+    each rank, select_rank_keys), in key order."""
+    import torch
+    return torch.sort(torch.cat([select_rank_keys(route, r, n) for r in range(world)])).values
+
+
 def reduce_over_ranks(times, sums, world, device):
     """Max over ranks of the step times, sum over ranks of the byte / error counters."""
     import torch

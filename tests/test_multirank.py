@@ -85,6 +85,70 @@ def test_two_rank_partition_and_reduction():
     assert sums == [float(world * n * 1024), 14.0, 1.0]
 
 
+def _rows_of(keys, vlen):
+    import torch
+    k = torch.as_tensor(keys, dtype=torch.int64).view(-1, 1)
+    return ((k * 131 + torch.arange(vlen, dtype=torch.int64).view(1, -1) * 7) % 251).to(torch.uint8)
+
+
+def _scatter_worker(rank, world, port, n, vlen, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "poor-man-s-cache_amd")]
+    import torch
+    import torch.distributed as dist
+    import bench
+    from pmc_codec import scatter as S
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        route = torch.from_numpy(_route_cpu(bench.route_span(n, world), world))
+        packed = tags = counts = None
+        if rank == 0:  # the landing batch: every rank's keys, in key order, resident on the landing rank
+            landing = bench.landing_keys(route, world, n)
+            packed, order, counts = S.pack_by_owner(_rows_of(landing, vlen), route[landing], world)
+            tags = landing[order]
+        rows, got = S.scatter_rows(packed, tags, counts, vlen, device=torch.device("cpu"))
+        want = bench.select_rank_keys(route, rank, n)
+        q.put((rank, bool(torch.equal(got, want)), bool(torch.equal(rows, _rows_of(want, vlen))), int(got.numel())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_landing_batch_scattered_to_owners(world):
+    """A batch resident on rank 0 (bench.py --landing scatter) reaches each owner rank as exactly the keys (and
+    value rows) that rank would have selected itself -- the same partition as the no-collective path, so the
+    per-rank reference digests still apply -- through pack_by_owner + one all-to-all (gloo here, RCCL on GPUs)."""
+    import torch.multiprocessing as mp
+    n, vlen = 700, 40
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, n, vlen, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted(q.get(timeout=240) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert res == [(r, True, True, n) for r in range(world)]
+
+
+def test_pack_by_owner_keeps_batch_order():
+    import torch
+    sys.path[:0] = [os.path.join(ROOT, "poor-man-s-cache_amd")]
+    from pmc_codec import scatter as S
+    owner = torch.tensor([2, 0, 1, 0, 2, 2, 1, 0], dtype=torch.uint8)
+    vals = torch.arange(8, dtype=torch.uint8).view(-1, 1).repeat(1, 3)
+    packed, order, counts = S.pack_by_owner(vals, owner, 3)
+    assert counts.tolist() == [3, 2, 3]
+    assert order.tolist() == [1, 3, 7, 2, 6, 0, 4, 5]
+    assert packed[:, 0].tolist() == order.tolist()
+    with pytest.raises(ValueError):
+        S.pack_by_owner(vals, owner, 2)
+
+
 def test_route_span_covers_every_world():
     import bench
     for world in (1, 2, 4, 8):
