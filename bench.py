@@ -83,6 +83,10 @@ def parse():
     ap.add_argument("--batches", action="store_true",
                     help="server-shaped batches (256 / 1,024 / 4,096 / 400 values, default 4 KiB): ms per batch")
     ap.add_argument("--mix-keys", type=int, default=1_000_000)
+    ap.add_argument("--landing", choices=["host", "scatter"], default="host",
+                    help="scatter: the whole batch lands in rank 0's HBM and is scattered to its owner GPUs by one "
+                         "RCCL all-to-all before the timed steps (SURVEY §8e); host (default): each rank generates "
+                         "its own share, no collective")
     ap.add_argument("--mix-serial", action="store_true", help="SETs and GETs of a batch on one stream")
     ap.add_argument("--mix-ops", type=int, default=1_048_576)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06", "traffic.json"),
@@ -479,7 +483,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if args.landing == "scatter" and world == 1 and "MASTER_ADDR" not in os.environ:
+        import socket
+        with socket.socket() as so:  # a one-rank RCCL group, so the scatter's collectives run as at N > 1
+            so.bind(("127.0.0.1", 0))
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(so.getsockname()[1]), RANK="0", WORLD_SIZE="1")
+    distributed = world > 1 or args.landing == "scatter"
+    if distributed:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -501,19 +511,28 @@ def main():
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
     # ---- this rank's keys: route "key"+i to GPUs, take the first n routed here -----------
-    if world > 1:
+    landing = None
+    if world > 1 or args.landing == "scatter":
         span = route_span(n, world)
         route = torch.empty(span, dtype=torch.uint8, device=dev)
         assert L.pmc_route_keys(0, span, NUM_SHARDS, world, route.data_ptr(), sh) == 0
         index = select_rank_keys(route, rank, n)
-        del route
         idx_ptr = index.data_ptr()
     else:
         index, idx_ptr = None, None
     corpus = torch.frombuffer(bytearray(corpus_b), dtype=torch.uint8).to(dev)
     src = torch.empty(n * vlen + 16, dtype=torch.uint8, device=dev)
-    assert L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), seed, args.kind, 0, idx_ptr, n, vlen,
-                            src.data_ptr(), sh) == 0
+    if args.landing == "scatter":
+        landing = scatter_landing(L, args, route, corpus, len(corpus_b), seed, world, rank, n, vlen, dev, sh)
+        src[:n * vlen].copy_(landing.pop("rows").view(-1))
+        landing["tags_match"] = bool(torch.equal(landing.pop("tags"), index))
+        if not landing["tags_match"]:
+            raise RuntimeError(f"rank {rank}: the scattered keys are not the ones this rank owns")
+    else:
+        assert L.pmc_gen_values(corpus.data_ptr(), len(corpus_b), seed, args.kind, 0, idx_ptr, n, vlen,
+                                src.data_ptr(), sh) == 0
+    if index is not None:
+        del route
     off = torch.arange(n, dtype=torch.int64, device=dev) * vlen
     lens = torch.full((n,), vlen, dtype=torch.int32, device=dev)
     cap = pmc_codec.gzip_bound(vlen)
@@ -541,7 +560,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
@@ -549,7 +568,7 @@ def main():
     for k in range(args.steps):
         step(evs[k])
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -668,14 +687,49 @@ def main():
         }
         if h2h:
             out["host_to_host"] = h2h
+        if landing:
+            out["landing"] = landing
+            out["config"]["parallelism"] = f"shard-partitioned x{world}; batch landed on rank 0, one all-to-all"
         print(json.dumps(out), flush=True)
         # a guard that fired means values silently took the slow retry kernel: fail the run loudly (the
         # line above still records the counts); large periodic values may legitimately take the stitch's
         # fallback (guard_counts.retry), small ones never
         assert guards["sort"] == 0 and guards["codes"] == 0 and guards["probe"] == 0, guards
         assert vlen > 31808 or guards["retry"] == 0, guards
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
+
+
+def scatter_landing(L, args, route, corpus, corpus_len, seed, world, rank, n, vlen, dev, sh):
+    """--landing scatter: rank 0 generates the batch of every rank's keys (landing_keys: key order) in its HBM,
+    packs it by owner GPU on the device and one RCCL all-to-all over xGMI gives each rank its share
+    (pmc_codec.scatter).  Timed between barriers; returns the rank's rows and keys and the scatter's figures."""
+    import torch
+    import torch.distributed as dist
+    from pmc_codec import scatter as S
+    packed = tags = counts = None
+    if rank == 0:
+        keys = landing_keys(route, world, n)
+        batch = torch.empty(keys.numel() * vlen + 16, dtype=torch.uint8, device=dev)
+        assert L.pmc_gen_values(corpus.data_ptr(), corpus_len, seed, args.kind, 0, keys.data_ptr(), keys.numel(),
+                                vlen, batch.data_ptr(), sh) == 0
+        owner = route[keys]
+        packed, order, counts = S.pack_by_owner(batch[:keys.numel() * vlen].view(-1, vlen), owner, world)
+        tags = keys[order]
+        del batch, owner, order
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rows, got = S.scatter_rows(packed, tags, counts, vlen, device=dev)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    moved = n * world * vlen
+    return {"mode": "scatter", "root": 0, "bytes": moved, "ms": t * 1e3, "gib_s": moved / t / 2 ** 30,
+            "note": "one all-to-all of the landing batch (uint8 rows) plus its int64 keys; the timed steps then "
+                    "run on each rank's received share", "rows": rows, "tags": got}
 
 
 def host_to_host(ctx, src, off, lens, comp, coff, ccap, clen, crc, back, blen, brc, n, vlen, cstride, stream,
