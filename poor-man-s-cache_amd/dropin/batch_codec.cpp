@@ -3,6 +3,8 @@
 // /root/reference/src/kvs/kvs.cpp:148,182-196 (SET) and :224,233-234 (GET).
 #include "batch_codec.hpp"
 
+#include <sys/mman.h>
+
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -222,6 +224,155 @@ uint64_t fingerprint(const char *p, size_t n) {
 
 } // namespace
 
+// ---- device-store mode (f2 inside the unchanged kvs) ------------------------------------------------
+namespace {
+struct Handle {       // what Entry.value holds for a compressed value in store mode (vSize = 32)
+    char magic[4];    // "PMCX": a gzip member starts 1f 8b, so the two never look alike
+    uint32_t gen;     // allocation generation: a slot reused for another value never matches a primed one
+    pmc_extent ext;   // the member's extent in the device heap
+};
+static_assert(sizeof(Handle) == 32, "handle size");
+constexpr char kHandleMagic[4] = {'P', 'M', 'C', 'X'};
+constexpr size_t kHandleSlots = size_t(1) << 26;  // 64M values: 2 GiB of address space, touched as used
+
+struct StoreState {
+    bool on = false;
+    uint64_t heap_bytes = 0;
+    std::once_flag once;
+    pmc_store *store = nullptr;
+    char *slab = nullptr;  // kHandleSlots x 32 B, mapped at EnableDeviceStore
+    std::mutex mu;         // slots (SETs on the request thread, frees from kvs on the same thread, EndBatch)
+    std::vector<uint32_t> free_slots;
+    uint32_t next = 0, gen = 0;
+    size_t live = 0;
+};
+StoreState g_store;
+
+pmc_store *the_store() {
+    std::call_once(g_store.once, [] {
+        pmc_ctx *ctx = pmc_default_ctx();
+        if (!ctx || pmc_store_create(ctx, g_store.heap_bytes, &g_store.store) != PMC_OK) g_store.store = nullptr;
+    });
+    return g_store.store;
+}
+
+bool in_slab(const void *p) {
+    return g_store.slab && (const char *)p >= g_store.slab && (const char *)p < g_store.slab + kHandleSlots * 32;
+}
+
+char *handle_new(const pmc_extent &e) {
+    std::lock_guard<std::mutex> lk(g_store.mu);
+    uint32_t s;
+    if (!g_store.free_slots.empty()) {
+        s = g_store.free_slots.back();
+        g_store.free_slots.pop_back();
+    } else if (g_store.next < kHandleSlots) {
+        s = g_store.next++;
+    } else {
+        return nullptr;
+    }
+    Handle *h = (Handle *)(g_store.slab + (size_t)s * 32);
+    memcpy(h->magic, kHandleMagic, 4);
+    h->gen = ++g_store.gen;
+    h->ext = e;
+    g_store.live++;
+    return (char *)h;
+}
+
+// the extent a live handle names (false: not a handle of this store)
+bool handle_extent(const char *p, size_t n, pmc_extent *e) {
+    if (n != sizeof(Handle) || !in_slab(p) || ((uintptr_t)(p - g_store.slab) & 31)) return false;
+    const Handle *h = (const Handle *)p;
+    if (memcmp(h->magic, kHandleMagic, 4) != 0 || !(h->ext.flags & 1)) return false;
+    *e = h->ext;
+    return true;
+}
+
+// extents of the handles collected by a dry run, decoded in one store call: out[k] a new[] NUL-terminated
+// value of olen[k] bytes, or nullptr
+void store_get(const std::vector<pmc_extent> &ext, std::vector<char *> &out, std::vector<uint32_t> &olen) {
+    const size_t n = ext.size();
+    out.assign(n, nullptr);
+    olen.assign(n, 0);
+    pmc_store *st = the_store();
+    if (!n || !st) return;
+    std::vector<const uint8_t *> resp(n, nullptr);
+    std::vector<uint32_t> rlen(n, 0);
+    std::vector<int32_t> rc(n, 0);
+    if (pmc_store_get_batch(st, ext.data(), (uint32_t)n, PMC_FRAME_RAW, resp.data(), rlen.data(), rc.data()) != PMC_OK)
+        return;
+    for (size_t k = 0; k < n; k++) {
+        if (rc[k] != PMC_OK || !resp[k]) continue;
+        char *v = new char[rlen[k] + 1];
+        memcpy(v, resp[k], rlen[k]);
+        v[rlen[k]] = '\0';
+        out[k] = v;
+        olen[k] = rlen[k];
+    }
+}
+}  // namespace
+
+void EnableDeviceStore(uint64_t heap_bytes) {
+    if (g_store.on) return;
+    void *m = mmap(nullptr, kHandleSlots * 32, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (m == MAP_FAILED) return;
+    g_store.slab = (char *)m;
+    g_store.heap_bytes = heap_bytes;
+    g_store.on = true;
+}
+
+namespace detail {
+bool StoreMode() { return g_store.on; }
+
+bool ReleaseIfHandle(void *p) noexcept {
+    if (!in_slab(p)) return false;  // (checked before any lock: the store's own frees come through here too)
+    std::lock_guard<std::mutex> lk(g_store.mu);
+    Handle *h = (Handle *)p;
+    if (memcmp(h->magic, kHandleMagic, 4) == 0) {
+        if ((h->ext.flags & 1) && g_store.store) pmc_store_free(g_store.store, &h->ext, 1);
+        memset(h, 0, sizeof *h);
+        g_store.free_slots.push_back((uint32_t)(((char *)p - g_store.slab) / 32));
+        g_store.live--;
+    }
+    return true;
+}
+
+bool StoreCompress(const char *input, size_t len, CompressResult *out) {
+    if (!g_store.on) return false;
+    pmc_store *st = the_store();
+    const uint64_t off = 0;
+    const uint32_t l = (uint32_t)len;
+    pmc_extent e{};
+    int32_t rc = PMC_E_NO_DEVICE;
+    if (st) {
+        const int r = pmc_store_put_batch(st, (const uint8_t *)input, &off, &l, 1, &e, &rc);
+        if (r) rc = r;
+    }
+    if (rc != PMC_OK) {
+        *out = {nullptr, 0, rc};  // kvs stores the raw value (kvs.cpp:188-192)
+        return true;
+    }
+    char *h = handle_new(e);
+    if (!h) {
+        pmc_store_free(st, &e, 1);
+        *out = {nullptr, 0, PMC_Z_MEM_ERROR};
+        return true;
+    }
+    *out = {h, sizeof(Handle), OPERATION_SUCCESS};
+    return true;
+}
+
+bool StoreDecompress(const char *input, size_t size, DecompressResult *out) {
+    pmc_extent e;
+    if (!g_store.on || !handle_extent(input, size, &e)) return false;
+    std::vector<char *> v;
+    std::vector<uint32_t> n;
+    store_get({e}, v, n);
+    *out = v[0] ? DecompressResult{v[0], OPERATION_SUCCESS} : DecompressResult{nullptr, PMC_Z_DATA_ERROR};
+    return true;
+}
+}  // namespace detail
+
 // One compress batch: its arrays (built on the request thread) and its results; run() touches nothing
 // else, so it may run on a helper thread (PrimeCompressAsync) while the request thread does the GETs.
 struct CompressJob {
@@ -229,6 +380,7 @@ struct CompressJob {
     std::vector<uint32_t> src_len, dst_cap, dst_len;
     std::vector<int32_t> rc;
     std::vector<uint8_t> dst;
+    std::vector<pmc_extent> ext;  // store mode: the members' extents
     const char *vals = nullptr;
     int r = PMC_OK;
     bool build(PrimeState &P, const std::vector<std::string_view> &values) {
@@ -249,6 +401,14 @@ struct CompressJob {
         return !src_len.empty();
     }
     void run(pmc_ctx *ctx) {
+        if (g_store.on) {  // the members go straight into HBM extents; only their handles come back
+            pmc_store *st = the_store();
+            ext.assign(src_len.size(), pmc_extent{});
+            r = st ? pmc_store_put_batch(st, (const uint8_t *)vals, src_off.data(), src_len.data(),
+                                         (uint32_t)src_len.size(), ext.data(), rc.data())
+                   : PMC_E_NO_DEVICE;
+            return;
+        }
         r = ctx ? pmc_gzip_compress_batch_host(ctx, (const uint8_t *)vals, src_off.data(), src_len.data(),
                                                (uint32_t)src_len.size(), dst.data(), dst_off.data(), dst_cap.data(),
                                                dst_len.data(), rc.data())
@@ -258,18 +418,29 @@ struct CompressJob {
         P.stats.batches++;
         for (size_t k = 0; k < src_len.size(); k++) {
             if (r || rc[k] != OPERATION_SUCCESS) continue;  // not primed: Compress runs (and fails) itself
-            char *d = new char[dst_len[k]];
-            memcpy(d, dst.data() + dst_off[k], dst_len[k]);
+            char *d;
+            size_t dsize = dst_len.empty() ? 0 : dst_len[k];
+            if (g_store.on) {  // a handle per value; a second SET of the same value in the batch gets its own
+                d = handle_new(ext[k]);  // extent through the single-value path (no spare)
+                dsize = sizeof(Handle);
+                if (!d) {
+                    pmc_store_free(the_store(), &ext[k], 1);
+                    continue;
+                }
+            } else {
+                d = new char[dsize];
+                memcpy(d, dst.data() + dst_off[k], dsize);
+            }
             const uint32_t idx = (uint32_t)P.comp.size();
             const uint64_t fp = fingerprint(P.cvals.data() + src_off[k], src_len[k]);
             bool dup = false;  // (an equal value earlier in the batch: both keep their member bytes)
             auto range = P.cidx.equal_range(fp);
-            for (auto it = range.first; it != range.second; ++it) {
+            for (auto it = range.first; it != range.second && !g_store.on; ++it) {
                 auto &c = P.comp[it->second];
                 if (c.len == src_len[k] && memcmp(P.cvals.data() + c.off, P.cvals.data() + src_off[k], c.len) == 0)
                     c.dup = dup = true;
             }
-            P.comp.push_back({src_off[k], src_len[k], d, dst_len[k], {}, dup});
+            P.comp.push_back({src_off[k], src_len[k], d, dsize, {}, dup});
             P.cidx.emplace(fp, idx);
         }
     }
@@ -353,13 +524,30 @@ void PrimeCollected(pmc_ctx *ctx) {
     // with the values, no strlen over them)
     std::vector<uint64_t> off;
     std::vector<uint32_t> len;
-    for (uint32_t idx : which) {
-        off.push_back(P.dec[idx].off);
-        len.push_back((uint32_t)P.dec[idx].size);
+    std::vector<pmc_extent> hext;  // store mode: handles' extents, decoded by one store call
+    std::vector<uint32_t> hpos, mpos;
+    for (size_t k = 0; k < which.size(); k++) {
+        const PrimeState::Dec &d = P.dec[which[k]];
+        pmc_extent e;
+        if (g_store.on && handle_extent(P.dmembers.data() + d.off, d.size, &e)) {
+            hext.push_back(e);
+            hpos.push_back((uint32_t)k);
+        } else {
+            off.push_back(d.off);
+            len.push_back((uint32_t)d.size);
+            mpos.push_back((uint32_t)k);
+        }
     }
-    std::vector<char *> vals;
-    std::vector<uint32_t> olen;
-    decompress_packed((const uint8_t *)P.dmembers.data(), off, len, vals, olen, ctx);
+    std::vector<char *> vals(which.size(), nullptr), part;
+    std::vector<uint32_t> olen(which.size(), 0), plen;
+    if (!mpos.empty()) {
+        decompress_packed((const uint8_t *)P.dmembers.data(), off, len, part, plen, ctx);
+        for (size_t j = 0; j < mpos.size(); j++) vals[mpos[j]] = part[j], olen[mpos[j]] = plen[j];
+    }
+    if (!hpos.empty()) {
+        store_get(hext, part, plen);
+        for (size_t j = 0; j < hpos.size(); j++) vals[hpos[j]] = part[j], olen[hpos[j]] = plen[j];
+    }
     P.stats.batches++;
     for (size_t k = 0; k < which.size(); k++) {
         auto &d = P.dec[which[k]];
@@ -374,7 +562,9 @@ void PrimeCollected(pmc_ctx *ctx) {
 
 void EndBatch() {
     PrimeState &P = g_prime;
-    for (auto &c : P.comp) delete[] c.data;
+    for (auto &c : P.comp) {
+        if (c.data && !detail::ReleaseIfHandle(c.data)) delete[] c.data;  // (a handle nobody took: its extent too)
+    }
     for (auto &d : P.dec) delete[] d.data;
     P.cvals.clear();
     P.comp.clear();
@@ -386,7 +576,17 @@ void EndBatch() {
     P.didx.clear();
 }
 
-PrimeStats GetPrimeStats() { return g_prime.stats; }
+PrimeStats GetPrimeStats() {
+    PrimeStats s = g_prime.stats;
+    if (g_store.on && g_store.store) {
+        uint64_t used = 0, reserved = 0, heap = 0;
+        pmc_store_stats(g_store.store, &used, &reserved, &heap);
+        std::lock_guard<std::mutex> lk(g_store.mu);
+        s.store_values = g_store.live;
+        s.store_bytes = used;
+    }
+    return s;
+}
 
 namespace detail {
 

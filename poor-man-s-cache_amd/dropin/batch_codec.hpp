@@ -11,6 +11,7 @@
 // pmc_gzip_*_batch_host call each.
 #pragma once
 #include <cstddef>
+#include <cstdint>
 #include <string_view>
 #include <vector>
 
@@ -86,8 +87,28 @@ void EndBatch();
 /// found no primed result (ran the single-value path).
 struct PrimeStats {
     size_t compress_hits, compress_misses, decompress_hits, decompress_misses, batches;
+    size_t store_values;   ///< device-store mode: compressed values held in HBM now (live handles)
+    uint64_t store_bytes;  ///< ... and the heap bytes their members use
 };
 PrimeStats GetPrimeStats();
+
+// ---- f2 inside the UNCHANGED kvs: compressed values held in HBM ---------------------------------------
+// Device-store mode (a server that calls EnableDeviceStore before its first request): Compress returns,
+// instead of the gzip member, a 32-byte handle naming the member's extent in a device store (pmc_store_*),
+// and kvs keeps that handle as Entry.value / vSize with compressed = true (kvs.cpp:185-187).  Decompress of a
+// handle decodes the extent on the device.  The batch priming above works unchanged (the SET batch is one
+// pmc_store_put_batch, the GET dry run's handles one pmc_store_get_batch).  Handles live in a slab of their
+// own, so the server's replacement of operator delete[] (kvs frees Entry.value with delete[],
+// kvs.hpp:87-98) recognises one by its address and releases its extent: ReleaseIfHandle.
+void EnableDeviceStore(uint64_t heap_bytes);
+
+namespace detail {
+bool StoreMode();
+/// p inside the handle slab: release its extent and slot, return true (else false: not a handle)
+bool ReleaseIfHandle(void *p) noexcept;
+bool StoreCompress(const char *input, size_t len, CompressResult *out);
+bool StoreDecompress(const char *input, size_t size, DecompressResult *out);
+} // namespace detail
 
 namespace detail {
 // used by GzipCompressor (gzip_compressor.cpp)

@@ -21,6 +21,7 @@ CompressResult GzipCompressor::Compress(const char *input) {
     const size_t len = strlen(input);
     CompressResult primed;
     if (pmc_batch::detail::TakeCompressed(input, len, &primed)) return primed;  // batch-primed (f1)
+    if (pmc_batch::detail::StoreCompress(input, len, &primed)) return primed;   // device-store mode (f2)
     const size_t cap = pmc_gzip_bound(len);
     char *out = new char[cap];
     size_t n = 0;
@@ -37,6 +38,7 @@ DecompressResult GzipCompressor::Decompress(const char *input, size_t input_size
     if (pmc_batch::detail::Collecting(input, input_size)) return {nullptr, INVALID_INPUT};  // dry run
     DecompressResult primed;
     if (pmc_batch::detail::TakeDecompressed(input, input_size, &primed)) return primed;  // batch-primed
+    if (pmc_batch::detail::StoreDecompress(input, input_size, &primed)) return primed;   // a device-store handle
     // First guess: the ISIZE trailer (the input's last 4 bytes), clamped to DEFLATE's 1032:1
     // maximum expansion.  Bytes after the member (the reference ignores them, gzip_compressor.cpp:96)
     // make that guess wrong; the codec then reports PMC_E_CAPACITY with the decoded size and the

@@ -181,10 +181,10 @@ void write_stats() {
                      "\"decompress_hits\": %zu, \"decompress_misses\": %zu, \"ms\": {\"peek\": %.1f, "
                      "\"set_batch\": %.1f, \"get_dry_run\": %.1f, \"get_batch\": %.1f, \"iterations\": %.1f, "
                      "\"first_set_batch\": %.1f, \"first_get_batch\": %.1f}, "
-                     "\"set_values\": %zu, \"get_keys\": %zu}\n",
+                     "\"set_values\": %zu, \"get_keys\": %zu, \"store_values\": %zu, \"store_bytes\": %llu}\n",
                      g_last.batches, g_last.compress_hits, g_last.compress_misses, g_last.decompress_hits,
                      g_last.decompress_misses, g_t.peek, g_t.set, g_t.dry, g_t.get, g_t.iter, g_t.set_first, g_t.get_first, g_t.set_values,
-                     g_t.get_keys);
+                     g_t.get_keys, g_last.store_values, (unsigned long long)g_last.store_bytes);
         std::fclose(f);
     }
 }

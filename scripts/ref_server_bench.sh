@@ -6,6 +6,7 @@
 #           (server.cpp:631-643) -- the CPU baseline of this config, timed on this host
 #   dropin  the drop-in GzipCompressor, one GPU call per value
 #   batch   the drop-in + the f1 batch hook (one device batch per direction per epoll iteration)
+#   store   the batch build with kvs holding compressed values in HBM (f2, ref_store_hook.cpp)
 #   nocodec the same server with ENABLE_COMPRESSION=false: its request path alone
 # No connection before a server prints its ready line; pmc_loadgen then waits (10 s) until it answers
 # and writes 20 ms after connecting, which keeps clear of the reference's connect race (INTEGRATION.md
@@ -66,6 +67,7 @@ while read -r shape; do
     if want ref_zlib; then case_ ref_zlib ref_server zlib || exit 1; fi
     if want ref_nocodec; then ALLOW_MISMATCH=1 case_ ref_nocodec ref_nocodec none || exit 1; fi
     if want ref_batch; then case_ ref_batch ref_server batch || exit 1; fi
+    if want ref_store; then case_ ref_store ref_server store || exit 1; fi
     if want pmc_batch; then case_ pmc_batch pmc_srv batch || exit 1; fi
     if want pmc_off; then case_ pmc_off pmc_srv off || exit 1; fi
 done <<< "${SHAPES:-4096 16 8192 40000

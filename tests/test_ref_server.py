@@ -180,7 +180,7 @@ def _race_shaped(rc, rps):
     return len(fails) == 4 and all(f <= RACE_MAX_FAILURES for f in fails)
 
 
-@pytest.mark.parametrize("kind", ["zlib", "dropin", "batch"])
+@pytest.mark.parametrize("kind", ["zlib", "dropin", "batch", "store"])
 def test_reference_load_test_passes(kind):
     """tcp_server_test.py -p -b 100 verbatim (BASELINE configs[4]); it exits 1 on any failed request.
     Each attempt is bounded (60 s, a passing run takes ~3 s).  The reference's connect race
@@ -220,7 +220,7 @@ def test_reference_load_test_passes(kind):
                  f"{_zlib_attempts}")
 
 
-@pytest.mark.parametrize("kind", ["dropin", "batch"])
+@pytest.mark.parametrize("kind", ["dropin", "batch", "store"])
 def test_protocol_answers_equal_reference_server(golden, kind):
     """The same command sequences give the same answers from the reference server over zlib and over the
     drop-in (test_server._semantics encodes them; here checked against the real server).  Without a GPU
@@ -248,12 +248,16 @@ def test_resp_answers_are_the_reference_servers(golden):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["dropin", "batch"])
+@pytest.mark.parametrize("kind", ["dropin", "batch", "store"])
 def test_reference_server_on_gpu_codec(golden, tmp_path, kind):
+    """store: the batch build with the reference's kvs holding compressed values in HBM (ref_store_hook.cpp:
+    Entry.value is a handle to a device extent; delete[] of a handle releases the extent)."""
     s = RefServer(kind, tmp_path)
     try:
+        if kind == "store":  # RESP too: every reply the reference's own over zlib gives (test above)
+            resp_semantics(s.port, golden)
         _semantics(s.port, golden)
-        res = _load(s.port, 4096, 40_000 if kind == "batch" else 4_000, keys=8192 if kind == "batch" else 1024)
+        res = _load(s.port, 4096, 4_000 if kind == "dropin" else 40_000, keys=1024 if kind == "dropin" else 8192)
         # the JSON files through GET after the load: stored members decode to the reference's bytes
         files = [d for _, d in golden.data_files]
         assert _exchange(s.port, [b"SET f%d " % i + d for i, d in enumerate(files)]) == [b"OK"] * len(files)
@@ -261,7 +265,9 @@ def test_reference_server_on_gpu_codec(golden, tmp_path, kind):
     finally:
         st = s.stop()
     print(kind, res, st)
-    if kind == "batch":
+    if kind == "store":  # the values the load left stored sit in HBM: one extent per live key
+        assert st and st["store_values"] >= 8192 and st["store_bytes"] > 8192 * 500, st
+    if kind in ("batch", "store"):
         assert st and st["batches"] > 0 and st["compress_hits"] > 8192 and st["decompress_hits"] > 1000, st
         # misses are GETs of keys SET earlier in the same iteration (their entry is newer than the dry run)
         assert st["compress_misses"] == 0 and st["decompress_misses"] < st["decompress_hits"] // 4, st
