@@ -506,6 +506,8 @@ void PrimeCollected(pmc_ctx *ctx) {
     PrimeState &P = g_prime;
     P.collecting = false;
     std::vector<uint32_t> which;
+    std::vector<pmc_extent> hext;  // store mode: handles' extents, decoded by one store call
+    std::vector<uint32_t> hpos, mpos;
     for (const auto &c : P.collected) {
         auto seen = P.didx.find(c.first);
         if (seen != P.didx.end()) {  // one decode per stored member
@@ -516,6 +518,13 @@ void PrimeCollected(pmc_ctx *ctx) {
         P.didx.emplace(c.first, idx);
         P.dec.push_back({P.dmembers.size(), c.second, nullptr, 0, 0, {}, false});
         P.dmembers.append(c.first, c.second);
+        pmc_extent e;  // (the stored pointer itself: a handle is recognised by its address in the slab)
+        if (g_store.on && handle_extent(c.first, c.second, &e)) {
+            hext.push_back(e);
+            hpos.push_back((uint32_t)which.size());
+        } else {
+            mpos.push_back((uint32_t)which.size());
+        }
         which.push_back(idx);
     }
     P.collected.clear();
@@ -524,19 +533,9 @@ void PrimeCollected(pmc_ctx *ctx) {
     // with the values, no strlen over them)
     std::vector<uint64_t> off;
     std::vector<uint32_t> len;
-    std::vector<pmc_extent> hext;  // store mode: handles' extents, decoded by one store call
-    std::vector<uint32_t> hpos, mpos;
-    for (size_t k = 0; k < which.size(); k++) {
-        const PrimeState::Dec &d = P.dec[which[k]];
-        pmc_extent e;
-        if (g_store.on && handle_extent(P.dmembers.data() + d.off, d.size, &e)) {
-            hext.push_back(e);
-            hpos.push_back((uint32_t)k);
-        } else {
-            off.push_back(d.off);
-            len.push_back((uint32_t)d.size);
-            mpos.push_back((uint32_t)k);
-        }
+    for (uint32_t k : mpos) {
+        off.push_back(P.dec[which[k]].off);
+        len.push_back((uint32_t)P.dec[which[k]].size);
     }
     std::vector<char *> vals(which.size(), nullptr), part;
     std::vector<uint32_t> olen(which.size(), 0), plen;
