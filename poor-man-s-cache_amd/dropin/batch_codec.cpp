@@ -597,6 +597,7 @@ bool TakeCompressed(const char *input, size_t len, CompressResult *out) {
         auto &c = P.comp[it->second];
         if (c.len != len || memcmp(P.cvals.data() + c.off, input, len) != 0) continue;
         char *d = c.data;
+        if (!d && g_store.on) continue;  // store mode: an equal value later in the batch has its own extent
         if (!d && !c.dup) break;  // handed out, and no spare: the single-value path compresses it again
         if (d) {
             if (c.dup) c.spare.assign(d, c.size);
