@@ -270,4 +270,7 @@ def test_reference_server_on_gpu_codec(golden, tmp_path, kind):
     if kind in ("batch", "store"):
         assert st and st["batches"] > 0 and st["compress_hits"] > 8192 and st["decompress_hits"] > 1000, st
         # misses are GETs of keys SET earlier in the same iteration (their entry is newer than the dry run)
-        assert st["compress_misses"] == 0 and st["decompress_misses"] < st["decompress_hits"] // 4, st
+        # (store also ran resp_semantics: SETs queued by MULTI and run by EXEC are not primed, by design --
+        # ref_batch_hook.cpp -- and take the single-value path)
+        assert st["compress_misses"] <= (4 if kind == "store" else 0), st
+        assert st["decompress_misses"] < st["decompress_hits"] // 4, st
