@@ -129,10 +129,28 @@ def fullsize_parity(L, ctx, comp, coff, clen, n, vlen, kind, world, rank, sh):
                              sh) == 0
     rec = torch.stack([clen, mcrc], dim=1).cpu().numpy().astype("<u4")
     got = hashlib.sha256(rec.tobytes()).hexdigest()
-    return {"match": got == want["sha256"], "members": n, "sha256": got,
-            "method": "sha256 over the (u32 len, u32 CRC-32) record of every member, vs the reference's "
-                      "(a length + CRC-32 digest of the member bytes, not a byte-by-byte comparison; the "
-                      "byte-by-byte comparisons are the goldens, tests/test_gpu_codec.py)",
+    out = {"match": got == want["sha256"], "members": n, "sha256": got,
+           "method": "sha256 over the (u32 len, u32 CRC-32) record of every member, vs the reference's "
+                     "(a length + CRC-32 digest of the member bytes, not a byte-by-byte comparison; the "
+                     "byte-by-byte comparisons are the goldens, tests/test_gpu_codec.py)"}
+    if "bytes_sha256" in want:  # every member's bytes: compacted on the device, hashed on the host
+        t0 = time.perf_counter()
+        hb = hashlib.sha256()
+        stride = int(coff[1].item() - coff[0].item()) if n > 1 else int(clen[0].item())
+        if n > 1 and not bool((coff[1:] - coff[:-1] == stride).all()):
+            raise RuntimeError("members are not at a fixed stride")
+        rows = comp[int(coff[0].item()):int(coff[0].item()) + n * stride].view(n, stride)
+        col = torch.arange(stride, device=comp.device)[None, :]
+        for a in range(0, n, 1 << 20):
+            b = min(n, a + (1 << 20))
+            hb.update(rows[a:b][col < clen[a:b, None]].cpu().numpy().tobytes())
+        gotb = hb.hexdigest()
+        out.update(match=out["match"] and gotb == want["bytes_sha256"], bytes_sha256=gotb,
+                   bytes_match=gotb == want["bytes_sha256"], bytes_s=round(time.perf_counter() - t0, 2),
+                   method="sha256 over every member's BYTES back to back, and over the (u32 len, u32 CRC-32) "
+                          "records, each vs the reference's own Compress of the same values: a byte-by-byte "
+                          "check of every member")
+    return {**out,
             "reference": f"tests/golden/{fname} (reference GzipCompressor::Compress, zlib "
                          f"{doc.get('zlib_version')})"}
 

@@ -154,6 +154,9 @@ def ref():
         R.ref_bench.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(ctypes.c_uint64)]
+        R.ref_members.restype = ctypes.c_int
+        R.ref_members.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p,
+                                  ctypes.c_uint64, ctypes.c_void_p]
         R.ref_member_records.restype = ctypes.c_int
         R.ref_member_records.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                          ctypes.c_void_p, ctypes.c_void_p]
@@ -196,6 +199,21 @@ def member_records_digest(lens: np.ndarray, crcs: np.ndarray, h=None):
         h = hashlib.sha256()
     h.update(rec.tobytes())
     return h
+
+
+def ref_members_hash(values: np.ndarray, nthreads: int, h):
+    """The reference Compress over every row of `values`: its members' bytes, back to back in row order, go
+    into hashlib object h.  Returns the member lengths."""
+    R = ref()
+    n, vlen = values.shape
+    stride = bound(vlen)
+    dst = np.zeros((n, stride), np.uint8)
+    lens = np.zeros(n, np.uint32)
+    bad = R.ref_members(values.ctypes.data_as(ctypes.c_void_p), n, vlen, nthreads,
+                        dst.ctypes.data_as(ctypes.c_void_p), stride, lens.ctypes.data_as(ctypes.c_void_p))
+    assert bad == 0
+    h.update(dst[np.arange(stride)[None, :] < lens[:, None]].tobytes())
+    return lens
 
 
 def ref_member_records(values: np.ndarray, nthreads: int):

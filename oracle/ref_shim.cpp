@@ -99,4 +99,32 @@ int ref_member_records(const uint8_t *values, uint32_t n, uint32_t vlen, int nth
     for (auto &x : th) x.join();
     return bad.load();
 }
+
+// Byte-level full-size parity (make_full_digests.py --bytes): the reference's members themselves, member i
+// at dst + i * stride (stride >= the member's size), lens[i] its size.  Returns the number of failures.
+int ref_members(const uint8_t *values, uint32_t n, uint32_t vlen, int nthreads, uint8_t *dst, uint64_t stride,
+                uint32_t *lens) {
+    std::atomic<int> bad{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; t++)
+        th.emplace_back([&, t] {
+            std::vector<char> s(vlen + 1);
+            for (uint32_t i = t; i < n; i += nthreads) {
+                memcpy(s.data(), values + (uint64_t)i * vlen, vlen);
+                s[vlen] = 0;
+                CompressResult c = GzipCompressor::Compress(s.data());
+                if (c.operationResult != 0 || c.size > stride) {
+                    bad++;
+                    lens[i] = 0;
+                    delete[] c.data;
+                    continue;
+                }
+                lens[i] = (uint32_t)c.size;
+                memcpy(dst + (uint64_t)i * stride, c.data, c.size);
+                delete[] c.data;
+            }
+        });
+    for (auto &x : th) x.join();
+    return bad.load();
+}
 }

@@ -121,12 +121,56 @@ def rank_digests(corpus, threads):
         json.dump(doc, f, indent=1)
 
 
+def bytes_digests(corpus, threads):
+    """--bytes: SHA-256 over the reference's member BYTES, back to back in value order, for the north-star
+    workload at N = 1 (full_digests.json) and every rank of N = 2, 4, 8 (rank_digests.json), stored as
+    prefixes[n]["bytes_sha256"] beside the record digests.  bench.py compacts its members on the device and
+    hashes them on the host: a byte-by-byte check of all 10M members per GPU."""
+    n, vlen, kind, seed = SETS[0]
+    path = os.path.join(HERE, "full_digests.json")
+    with open(path) as f:
+        doc = json.load(f)
+    t0 = time.time()
+    h = hashlib.sha256()
+    for first in range(0, n, CHUNK):
+        O.ref_members_hash(O.gen_values(corpus, seed, kind, first, min(CHUNK, n - first), vlen), threads, h)
+    for st in doc["sets"]:
+        if (st["n"], st["vlen"], st["kind"]) == (n, vlen, kind):
+            st["prefixes"][str(n)]["bytes_sha256"] = h.hexdigest()
+    doc["bytes_record"] = "bytes_sha256: SHA-256 over the members' bytes, back to back in value order"
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=1)
+    print(f"N=1: {time.time() - t0:.1f} s", flush=True)
+    path = os.path.join(HERE, "rank_digests.json")
+    with open(path) as f:
+        rdoc = json.load(f)
+    for st in rdoc["sets"]:
+        t0 = time.time()
+        world, rank = st["world"], st["rank"]
+        route = O.route_keys(0, route_span(RANK_N, world), 128, world)
+        idx = np.nonzero(route == rank)[0][:RANK_N].astype(np.uint64)
+        assert hashlib.sha256(idx.astype("<u8").tobytes()).hexdigest() == st["index_sha256"]
+        h = hashlib.sha256()
+        for first in range(0, RANK_N, CHUNK):
+            O.ref_members_hash(O.gen_values_idx(corpus, 0x5EED, 0, idx[first:first + CHUNK], 1024), threads, h)
+        st["prefixes"][str(RANK_N)]["bytes_sha256"] = h.hexdigest()
+        print(f"world {world} rank {rank}: {time.time() - t0:.1f} s", flush=True)
+        with open(path, "w") as f:  # (after every rank: a long run keeps what it finished)
+            json.dump(rdoc, f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--bytes", action="store_true", help="add byte-level digests (bytes_digests)")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--ranks", action="store_true", help="only the per-rank digests (rank_digests.json)")
     ap.add_argument("--large", action="store_true", help="add the large-value bench legs to full_digests.json")
     args = ap.parse_args()
+    if args.bytes:
+        O.build(ref=True)
+        d = os.path.join(HERE, "data")
+        corpus = b"".join(open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d)) if f.endswith(".json"))
+        return bytes_digests(corpus, args.threads)
     if args.large:
         O.build(ref=True)
         d = os.path.join(HERE, "data")
