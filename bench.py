@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--batches", action="store_true",
                     help="server-shaped batches (256 / 1,024 / 4,096 / 400 values, default 4 KiB): ms per batch")
     ap.add_argument("--mix-keys", type=int, default=1_000_000)
+    ap.add_argument("--emulate", default="", metavar="RANK/WORLD",
+                    help="one GPU runs rank RANK's share of a WORLD-GPU run (its routed keys, checked against that "
+                         "rank's reference digests): rehearses the N > 1 parity path on a one-GPU box")
     ap.add_argument("--landing", choices=["host", "scatter"], default="host",
                     help="scatter: the whole batch lands in rank 0's HBM and is scattered to its owner GPUs by one "
                          "RCCL all-to-all before the timed steps (SURVEY §8e); host (default): each rank generates "
@@ -530,11 +533,14 @@ def main():
     sh = stream.cuda_stream
     # ---- this rank's keys: route "key"+i to GPUs, take the first n routed here -----------
     landing = None
-    if world > 1 or args.landing == "scatter":
-        span = route_span(n, world)
+    sel_rank, sel_world = (int(x) for x in args.emulate.split("/")) if args.emulate else (rank, world)
+    if args.emulate and (world > 1 or args.landing == "scatter" or not 0 <= sel_rank < sel_world):
+        raise SystemExit("--emulate RANK/WORLD: one process, default landing, 0 <= RANK < WORLD")
+    if sel_world > 1 or args.landing == "scatter":
+        span = route_span(n, sel_world)
         route = torch.empty(span, dtype=torch.uint8, device=dev)
-        assert L.pmc_route_keys(0, span, NUM_SHARDS, world, route.data_ptr(), sh) == 0
-        index = select_rank_keys(route, rank, n)
+        assert L.pmc_route_keys(0, span, NUM_SHARDS, sel_world, route.data_ptr(), sh) == 0
+        index = select_rank_keys(route, sel_rank, n)
         idx_ptr = index.data_ptr()
     else:
         index, idx_ptr = None, None
@@ -600,7 +606,9 @@ def main():
     torch.cuda.synchronize()
     bad = int(mism.item()) + int((crc != 0).sum().item()) + int((brc != 0).sum().item())
     comp_bytes = int(clen.to(torch.int64).sum().item())
-    parity = fullsize_parity(L, ctx, comp, coff, clen, n, vlen, args.kind, world, rank, sh)
+    parity = fullsize_parity(L, ctx, comp, coff, clen, n, vlen, args.kind, sel_world, sel_rank, sh)
+    if args.emulate and parity is not None:
+        parity["emulated"] = f"rank {sel_rank} of {sel_world}"
 
     (t_step_s, tc_max, td_max), (total_bytes, total_comp, total_bad, p_match, p_checked) = reduce_over_ranks(
         [wall / args.steps, tc, td], [float(n * vlen), float(comp_bytes), float(bad),
